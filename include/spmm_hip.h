@@ -1,0 +1,118 @@
+/*
+ * spmm_hip.h -- C ABI of the MI355X-native CSR SpMM engine (libspmm_hip.so).
+ *
+ * Drop-in boundary for the reference's per-format kernel plugin surface
+ * (reference: benchmark_code/CPU/AMD/spmv_code_bench/spmv_kernel.h:9-30, plugin spmm_kernel_csr.cpp:21-66).
+ * Plain pointers and sizes only; no C++ or torch types.  Every entry point returns an int status
+ * (SPMM_HIP_OK = 0, negative on error; spmm_hip_strerror() names it) where the reference returns void and
+ * exits on fatal errors (lib/debug.h:117,127) -- the C++ plugin shim converts a negative status into that exit.
+ *
+ * Layouts:
+ *   A    CSR, int32 row_ptr[m+1], int32 col_idx[nnz], values[nnz] (double or float), 0-based, columns sorted
+ *        per row as coo_to_csr leaves them (duplicates allowed).
+ *   B    the reference passes x = B COLUMN-major: column n at x[n*ncols .. +ncols) (spmm_kernel_csr.cpp:88).
+ *        The engine computes on a ROW-major device copy (B[col][K]); host column-major input is transposed on
+ *        the device, outside the SpMM kernel.
+ *   C    y = C ROW-major: y[i*K + n] (spmm_kernel_csr.cpp:93); every entry is written (0 for empty rows).
+ * Numerics: each C entry of a row with at most SPMM_HIP_SEQ_MAX nonzeros is one left-to-right fused
+ * multiply-add chain from 0 over the row's nonzeros in CSR order -- the same bits as the reference kernel built
+ * with its own flags on an FMA x86 host.  Longer rows are split into chunks whose partial sums are combined in a
+ * fixed order (deterministic run to run; within 1e-10 relative normwise for fp64).
+ */
+#ifndef SPMM_HIP_H
+#define SPMM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define SPMM_HIP_OK               0
+#define SPMM_HIP_ERR_ARG         -1   /* invalid argument (null pointer, negative size, bad enum)           */
+#define SPMM_HIP_ERR_NOMEM       -2   /* device or host allocation failed                                   */
+#define SPMM_HIP_ERR_HIP         -3   /* a HIP runtime call failed (details: spmm_hip_last_error_detail)     */
+#define SPMM_HIP_ERR_NODEVICE    -4   /* no HIP device / device index out of range                          */
+#define SPMM_HIP_ERR_K           -5   /* k does not match the k the handle was created for (see create)     */
+#define SPMM_HIP_ERR_CSR         -6   /* malformed CSR (row_ptr not monotone, col_idx out of [0, ncols))     */
+#define SPMM_HIP_ERR_OVERFLOW    -7   /* sizes exceed the engine's index range                              */
+
+/* value types (reference: -DValueType=double / float, make.sh:98-102) */
+#define SPMM_HIP_F64  0
+#define SPMM_HIP_F32  1
+
+/* B layouts for the device entry point */
+#define SPMM_HIP_B_COL_MAJOR  0   /* reference layout: x[n*ncols + col]                                    */
+#define SPMM_HIP_B_ROW_MAJOR  1   /* engine layout:   B[col*K + n]                                         */
+
+/* rows longer than this are split across workgroups (deterministic fixed-order combine) */
+#define SPMM_HIP_SEQ_MAX  4096
+
+typedef struct spmm_hip_handle spmm_hip_t;
+
+/* Factory: replaces `struct Matrix_Format *csr_to_format(INT_T *row_ptr, INT_T *col_ind, ValueType *values,
+ * long m, long n, long nnz, int k)` (spmv_kernel.h:29, spmm_kernel_csr.cpp:57-66).  Unlike the reference (which
+ * wraps the caller's arrays zero-copy and frees them in its destructor), the engine BORROWS the host arrays for
+ * the duration of the call only: it validates A, copies it to device `device`, and builds the workgroup block
+ * table (nnz-balanced row blocks).  k is the number of B columns the handle is planned for (0 = decide at the
+ * first run; any later run with a different k re-plans).  values points to double (SPMM_HIP_F64) or float. */
+int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *values, int64_t m, int64_t ncols,
+                    int64_t nnz, int32_t k, int32_t dtype, int32_t device, spmm_hip_t **out);
+
+/* Execute, host buffers: replaces `Matrix_Format::spmm(ValueType *x, ValueType *y, INT_T k)`
+ * (spmv_kernel.h:18, spmm_kernel_csr.cpp:51-54).  x = host B, column-major [k][ncols]; y = host C, row-major
+ * [m][k], overwritten.  Synchronous like the reference: uploads x (skipped when the environment variable
+ * SPMM_HIP_ASSUME_X_UNCHANGED=1 and x is the pointer of the previous call), transposes it on the device, runs
+ * the SpMM kernel, downloads y. */
+int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
+
+/* Execute, device buffers (kernel-only path; graph-capturable: no allocation or synchronisation inside once the
+ * handle is planned for this k and layout).  d_b: device B in `b_layout` (COL_MAJOR is transposed into an
+ * internal row-major buffer first, as a separate kernel); d_c: device C row-major [m][k].  stream: a hipStream_t
+ * (NULL = the null stream). */
+int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *d_c, int32_t k, void *stream);
+
+/* Plan for k without running (allocations happen here, not in run_device). */
+int spmm_hip_plan(spmm_hip_t *h, int32_t k);
+
+/* Timing of the LAST run on the handle, from HIP events recorded on the run's stream (blocks until the run
+ * finished): out_ms[0] = SpMM kernel(s) only, out_ms[1] = B transpose (0 if none), out_ms[2] = H2D of x,
+ * out_ms[3] = D2H of y (the last two only for spmm_hip_run). */
+int spmm_hip_last_times(spmm_hip_t *h, double *out_ms);
+
+/* Statistics: replaces statistics_print_labels / Matrix_Format::statistics_print_data
+ * (spmv_kernel.h:20,30; spmv_bench.cpp:441-443,474-476).  Appends CSV columns to buf (at most buf_n bytes incl.
+ * NUL) and returns the number of characters written (<0 on error).  Columns:
+ *   kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,long_rows,device */
+int spmm_hip_stats_labels(char *buf, long buf_n);
+int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
+
+/* Static properties of the handle: out[0]=m, out[1]=ncols, out[2]=nnz, out[3]=k planned, out[4]=dtype,
+ * out[5]=number of row blocks, out[6]=number of long-row chunks, out[7]=device bytes held. */
+int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
+
+/* Device buffers owned by the handle (for callers that stage B/C themselves), row-major B of the planned k. */
+int spmm_hip_device_ptrs(spmm_hip_t *h, void **d_b_rowmajor, void **d_c);
+
+int spmm_hip_destroy(spmm_hip_t *h);
+
+/* nnz-balanced row split (reference: loop_partitioner_balance_prefix_sums, lib/parallel_util.h:141-165, with
+ * binary_search lib/macros/macrolib.h:471-524): worker w of W gets rows [*start, *end).  Used for GPU shards. */
+int spmm_hip_partition_rows(const int32_t *row_ptr, int64_t m, int64_t nnz, int64_t num_workers,
+                            int64_t worker_pos, int64_t *start, int64_t *end);
+
+/* Algorithmic byte model per SpMM call (reference SpMV model spmv_operator.cu:30-32 extended to
+ * K columns): 4(m+1) + (4+s)nnz + s*K*ncols + s*K*m, s = sizeof(value). */
+double spmm_hip_bytes_alg(int64_t m, int64_t ncols, int64_t nnz, int32_t k, int32_t dtype);
+
+const char *spmm_hip_strerror(int status);
+const char *spmm_hip_last_error_detail(void);
+int spmm_hip_device_count(int *count);
+const char *spmm_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPMM_HIP_H */

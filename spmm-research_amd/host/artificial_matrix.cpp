@@ -1,0 +1,453 @@
+// artificial_matrix.cpp -- synthetic CSR generator (the reference's artificial-matrix-generator submodule is empty
+// in the reference tree, .gitmodules:5-8; this is a from-scratch design against its 11-parameter contract,
+// spmv_bench.cpp:842-869, and the feature definitions that measure it, csr_util_gen.c:269-610,964-983).
+//
+// Model, per row i (degree d_i):
+//   * d_i ~ |N(avg, std)| ("normal", lib/random.h random_normal: Box-Muller) or Gamma(k=(avg/std)^2,
+//     theta=std^2/avg) ("gamma", Marsaglia-Tsang), rounded, capped at nr_cols.
+//   * skew > 0: one row (seeded choice) gets degree avg*(1+skew) (capped at nr_cols); the other rows are scaled so
+//     that the total stays avg*nr_rows -- the feature skew = (max - avg)/avg then equals the parameter.
+//   * columns live in a window of width W_i = bw*nr_cols*(d+1)/(d-1) (the expected span of d uniform points in
+//     the window is then bw*nr_cols) centred on the diagonal; "random" placement = uniform positions inside it,
+//     "diagonal" = the same window with positions drawn from the central half (a tighter band).
+//   * neighbours: the row is laid out as R = d*(1 - nu/2) runs of consecutive columns separated by >= 1 free column;
+//     a run of length L contributes 2(L-1) to the row-neighbour count, so the mean over the row's nonzeros is nu.
+//   * cross-row similarity: row i copies whole runs of row i-1 until crs*d_{i-1} of row i-1's columns reappear
+//     (an exact copy is a neighbour at |dcol| = 0 <= 1); the rest of row i is new runs in its own window.
+//   * values: seeded uniform [0.5, 1.5) (positive, cancellation-free, so 1e-10 checks are meaningful).
+// Determinism: every random stream is keyed by (seed, row, purpose); the copy chain restarts every SEG rows so
+// segments can be generated independently (any thread count, any row range) with identical output.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/spmm_host.h"
+
+namespace {
+
+constexpr int64_t SEG = 4096;  // copy-chain restart period (rows)
+
+inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+struct Rng {  // xoshiro256**
+    uint64_t s[4];
+    Rng(uint64_t seed, uint64_t a, uint64_t b) {
+        uint64_t x = splitmix64(seed ^ splitmix64(a * 0x100000001B3ULL + b));
+        for (auto &v : s) v = x = splitmix64(x);
+    }
+    static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t next() {
+        const uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t; s[3] = rotl(s[3], 45);
+        return r;
+    }
+    double uniform() { return (next() >> 11) * 0x1.0p-53; }  // [0,1)
+    int64_t below(int64_t n) { return n <= 1 ? 0 : (int64_t)(uniform() * (double)n); }
+    double normal() {  // Box-Muller
+        double u1 = uniform(), u2 = uniform();
+        if (u1 < 1e-300) u1 = 1e-300;
+        return std::sqrt(-2.0 * std::log(u1)) * std::cos(2.0 * M_PI * u2);
+    }
+    double gamma(double k) {  // Marsaglia-Tsang, k > 0
+        if (k < 1.0) return gamma(k + 1.0) * std::pow(uniform() + 1e-300, 1.0 / k);
+        const double d = k - 1.0 / 3.0, c = 1.0 / std::sqrt(9.0 * d);
+        for (;;) {
+            double x, v;
+            do {
+                x = normal();
+                v = 1.0 + c * x;
+            } while (v <= 0);
+            v = v * v * v;
+            const double u = uniform();
+            if (u < 1.0 - 0.0331 * x * x * x * x) return d * v;
+            if (std::log(u) < 0.5 * x * x + d * (1.0 - v + std::log(v))) return d * v;
+        }
+    }
+};
+
+enum Stream : uint64_t { S_DEG = 1, S_SKEW = 2, S_COLS = 3, S_VALS = 4 };
+
+bool valid(const spmm_gen_params_t *p) {
+    return p && p->nr_rows > 0 && p->nr_cols > 0 && p->avg_nnz_per_row >= 0 && p->std_nnz_per_row >= 0 &&
+           p->bw >= 0 && p->skew >= 0 && p->avg_num_neighbours >= 0 && p->cross_row_similarity >= 0;
+}
+
+// Row degrees of the whole matrix (deterministic, thread-count independent).
+int row_degrees(const spmm_gen_params_t *p, std::vector<int64_t> &deg) {
+    const int64_t m = p->nr_rows, n = p->nr_cols;
+    const double avg = p->avg_nnz_per_row, sd = p->std_nnz_per_row;
+    const bool gam = (strcmp(p->distribution, "gamma") == 0);
+    std::vector<double> raw(m);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < m; ++i) {
+        Rng r((uint64_t)p->seed, (uint64_t)i, S_DEG);
+        double x;
+        if (gam && avg > 0 && sd > 0) {
+            const double k = (avg / sd) * (avg / sd), theta = sd * sd / avg;
+            x = r.gamma(k) * theta;
+        } else {
+            x = std::fabs(avg + sd * r.normal());
+        }
+        raw[i] = x;
+    }
+    deg.assign(m, 0);
+    int64_t giant = -1, giant_deg = 0;
+    double scale = 1.0;
+    if (p->skew > 0 && m > 1) {
+        Rng r((uint64_t)p->seed, 0, S_SKEW);
+        giant = r.below(m);
+        giant_deg = std::min<int64_t>(n, (int64_t)std::llround(avg * (1.0 + p->skew)));
+        double rest = 0;
+#pragma omp parallel for reduction(+ : rest)
+        for (int64_t i = 0; i < m; ++i)
+            if (i != giant) rest += raw[i];
+        const double want = std::max(0.0, avg * (double)m - (double)giant_deg);
+        scale = rest > 0 ? want / rest : 0.0;
+    }
+    int64_t total = 0;
+#pragma omp parallel for reduction(+ : total)
+    for (int64_t i = 0; i < m; ++i) {
+        int64_t d = (i == giant) ? giant_deg : (int64_t)std::llround(raw[i] * scale);
+        d = std::max<int64_t>(0, std::min<int64_t>(d, n));
+        deg[i] = d;
+        total += d;
+    }
+    if (total >= INT32_MAX) return SPMM_HOST_ERR_OVERFLOW;
+    return SPMM_HOST_OK;
+}
+
+struct RowGen {
+    const spmm_gen_params_t *p;
+    std::vector<int32_t> prev, cur, tmp;
+    std::vector<std::pair<int32_t, int32_t>> runs_prev, runs_cur;  // (start, length)
+
+    // window [lo, lo+W) for row i with degree d
+    void window(int64_t i, int64_t d, int64_t &lo, int64_t &W) const {
+        const int64_t n = p->nr_cols, m = p->nr_rows;
+        double w = p->bw * (double)n;
+        if (d >= 2) w *= (double)(d + 1) / (double)(d - 1);
+        W = std::max<int64_t>(std::llround(w), std::max<int64_t>(1, d));
+        // room for the runs and their separating gaps
+        W = std::min<int64_t>(n, std::max<int64_t>(W, 2 * d));
+        const double center = ((double)i + 0.5) * (double)n / (double)m;
+        lo = (int64_t)std::llround(center - 0.5 * (double)W);
+        lo = std::max<int64_t>(0, std::min<int64_t>(lo, n - W));
+        if (strcmp(p->placement, "diagonal") == 0 && W >= 4 * std::max<int64_t>(d, 1)) {
+            lo += W / 4;
+            W /= 2;
+        }
+    }
+
+    static bool taken(const std::vector<int32_t> &sorted, int64_t c) {
+        return std::binary_search(sorted.begin(), sorted.end(), (int32_t)c);
+    }
+
+    // Generate row i (degree d) given the previous row of the chain (prev/runs_prev, possibly empty).
+    void gen(int64_t i, int64_t d) {
+        cur.clear();
+        runs_cur.clear();
+        if (d == 0) return;
+        const int64_t n = p->nr_cols;
+        Rng r((uint64_t)p->seed, (uint64_t)i, S_COLS);
+        const double nu = std::min(2.0, p->avg_num_neighbours);
+
+        // 1. copy whole runs of the previous row
+        if (!runs_prev.empty() && p->cross_row_similarity > 0) {
+            int64_t target = std::llround(p->cross_row_similarity * (double)prev.size());
+            target = std::min<int64_t>(target, d);
+            std::vector<int> order(runs_prev.size());
+            for (size_t q = 0; q < order.size(); ++q) order[q] = (int)q;
+            for (size_t q = order.size(); q > 1; --q) std::swap(order[q - 1], order[r.below((int64_t)q)]);
+            int64_t got = 0;
+            for (int q : order) {
+                if (got >= target) break;
+                auto run = runs_prev[q];
+                // whole runs keep the neighbour structure; only the row's own capacity truncates one
+                int32_t len = (int32_t)std::min<int64_t>(run.second, d - got);
+                runs_cur.push_back({run.first, len});
+                for (int32_t t = 0; t < len; ++t) cur.push_back(run.first + t);
+                got += len;
+            }
+        }
+        std::sort(cur.begin(), cur.end());
+
+        // 2. new runs in the row's own window
+        int64_t rest = d - (int64_t)cur.size();
+        if (rest > 0) {
+            int64_t lo, W;
+            window(i, d, lo, W);
+            int64_t R = std::max<int64_t>(1, std::llround((double)rest * (1.0 - nu / 2.0)));
+            R = std::min<int64_t>(R, rest);
+            // run lengths: all 1, then the remaining units dealt at random
+            std::vector<int64_t> L(R, 1);
+            for (int64_t u = R; u < rest; ++u) L[r.below(R)]++;
+            const int64_t free_cells = W - rest - (R - 1);
+            std::vector<int64_t> g(R);
+            if (free_cells >= 0) {
+                for (auto &x : g) x = r.below(free_cells + 1);
+                std::sort(g.begin(), g.end());
+            }
+            int64_t off = 0;
+            tmp.clear();
+            for (int64_t q = 0; q < R; ++q) {
+                int64_t start = (free_cells >= 0) ? lo + g[q] + off + q : lo + r.below(std::max<int64_t>(1, W - L[q]));
+                off += L[q];
+                // keep the run clear of copied columns (exact hits or adjacency); retry a few random starts
+                for (int tries = 0; tries < 8; ++tries) {
+                    bool clash = false;
+                    for (int64_t t = -1; t <= L[q] && !clash; ++t) clash = taken(cur, start + t);
+                    if (!clash) break;
+                    start = lo + r.below(std::max<int64_t>(1, W - L[q]));
+                }
+                for (int64_t t = 0; t < L[q]; ++t) {
+                    const int64_t c = start + t;
+                    if (c >= 0 && c < n) tmp.push_back((int32_t)c);
+                }
+                runs_cur.push_back({(int32_t)start, (int32_t)L[q]});
+            }
+            cur.insert(cur.end(), tmp.begin(), tmp.end());
+            std::sort(cur.begin(), cur.end());
+            cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
+            // 3. top up after collisions: random free columns, window first, then the whole row
+            int64_t guard = 0;
+            while ((int64_t)cur.size() < d) {
+                const bool wide = guard++ > 64 * d;
+                const int64_t c = wide ? r.below(n) : lo + r.below(W);
+                if (!taken(cur, c)) cur.insert(std::upper_bound(cur.begin(), cur.end(), (int32_t)c), (int32_t)c);
+                if (guard > 4096 * d + 1000000) {  // dense row: take the first free columns
+                    for (int64_t c2 = 0; c2 < n && (int64_t)cur.size() < d; ++c2)
+                        if (!taken(cur, c2)) cur.insert(std::upper_bound(cur.begin(), cur.end(), (int32_t)c2), (int32_t)c2);
+                }
+            }
+        } else if ((int64_t)cur.size() > d) {
+            cur.resize(d);
+        }
+        // rebuild the run list from the final sorted columns (what the next row copies)
+        runs_cur.clear();
+        for (size_t q = 0; q < cur.size();) {
+            size_t t = q + 1;
+            while (t < cur.size() && cur[t] == cur[t - 1] + 1) ++t;
+            runs_cur.push_back({cur[q], (int32_t)(t - q)});
+            q = t;
+        }
+    }
+};
+
+int alloc_csr(spmm_csr_t *out, int64_t m, int64_t ncols, int64_t nnz) {
+    out->m = m;
+    out->ncols = ncols;
+    out->nnz = nnz;
+    out->row_ptr = (int32_t *)malloc((size_t)(m + 1) * sizeof(int32_t));
+    out->col_idx = (int32_t *)malloc((size_t)std::max<int64_t>(nnz, 1) * sizeof(int32_t));
+    out->values = (double *)malloc((size_t)std::max<int64_t>(nnz, 1) * sizeof(double));
+    if (!out->row_ptr || !out->col_idx || !out->values) {
+        spmm_host_csr_free(out);
+        return SPMM_HOST_ERR_NOMEM;
+    }
+    return SPMM_HOST_OK;
+}
+
+// Fill rows [r0, r1) (row_ptr already holds the rebased offsets of that range).
+void fill_rows(const spmm_gen_params_t *p, const std::vector<int64_t> &deg, int64_t r0, int64_t r1,
+               spmm_csr_t *out) {
+    const int64_t seg0 = r0 / SEG, seg1 = (r1 + SEG - 1) / SEG;
+#pragma omp parallel
+    {
+        RowGen g;
+        g.p = p;
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t s = seg0; s < seg1; ++s) {
+            g.prev.clear();
+            g.runs_prev.clear();
+            const int64_t a = s * SEG, b = std::min<int64_t>((s + 1) * SEG, p->nr_rows);
+            for (int64_t i = a; i < b; ++i) {
+                g.gen(i, deg[i]);
+                if (i >= r0 && i < r1) {
+                    const int64_t base = out->row_ptr[i - r0];
+                    Rng rv((uint64_t)p->seed, (uint64_t)i, S_VALS);
+                    for (size_t t = 0; t < g.cur.size(); ++t) {
+                        out->col_idx[base + t] = g.cur[t];
+                        out->values[base + t] = 0.5 + rv.uniform();
+                    }
+                }
+                if (!g.cur.empty()) {  // the chain links non-empty rows (csr_util_gen.c:570-572)
+                    std::swap(g.prev, g.cur);
+                    std::swap(g.runs_prev, g.runs_cur);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int spmm_host_parse_gen_line(const char *line, spmm_gen_params_t *p) {
+    if (!line || !p) return SPMM_HOST_ERR_ARG;
+    memset(p, 0, sizeof(*p));
+    long long rows, cols, seed;
+    char dist[16], place[16];
+    int n = sscanf(line, "%lld %lld %lf %lf %15s %15s %lf %lf %lf %lf %lld", &rows, &cols, &p->avg_nnz_per_row,
+                   &p->std_nnz_per_row, dist, place, &p->bw, &p->skew, &p->avg_num_neighbours,
+                   &p->cross_row_similarity, &seed);
+    if (n != 11) return SPMM_HOST_ERR_PARSE;
+    p->nr_rows = rows;
+    p->nr_cols = cols;
+    p->seed = seed;
+    snprintf(p->distribution, sizeof(p->distribution), "%s", dist);
+    snprintf(p->placement, sizeof(p->placement), "%s", place);
+    return SPMM_HOST_OK;
+}
+
+int spmm_host_generate_row_ptr(const spmm_gen_params_t *p, int32_t *row_ptr) {
+    if (!valid(p) || !row_ptr) return SPMM_HOST_ERR_ARG;
+    std::vector<int64_t> deg;
+    int st = row_degrees(p, deg);
+    if (st) return st;
+    row_ptr[0] = 0;
+    for (int64_t i = 0; i < p->nr_rows; ++i) row_ptr[i + 1] = (int32_t)(row_ptr[i] + deg[i]);
+    return SPMM_HOST_OK;
+}
+
+int spmm_host_generate_rows(const spmm_gen_params_t *p, int64_t r0, int64_t r1, spmm_csr_t *out) {
+    if (!valid(p) || !out || r0 < 0 || r1 < r0 || r1 > p->nr_rows) return SPMM_HOST_ERR_ARG;
+    memset(out, 0, sizeof(*out));
+    std::vector<int64_t> deg;
+    int st = row_degrees(p, deg);
+    if (st) return st;
+    int64_t nnz = 0;
+    for (int64_t i = r0; i < r1; ++i) nnz += deg[i];
+    st = alloc_csr(out, r1 - r0, p->nr_cols, nnz);
+    if (st) return st;
+    out->row_ptr[0] = 0;
+    for (int64_t i = r0; i < r1; ++i) out->row_ptr[i - r0 + 1] = (int32_t)(out->row_ptr[i - r0] + deg[i]);
+    fill_rows(p, deg, r0, r1, out);
+    return SPMM_HOST_OK;
+}
+
+int spmm_host_generate(const spmm_gen_params_t *p, spmm_csr_t *out) {
+    if (!valid(p)) return SPMM_HOST_ERR_ARG;
+    return spmm_host_generate_rows(p, 0, p->nr_rows, out);
+}
+
+int spmm_host_features(const spmm_csr_t *a, spmm_features_t *f) {
+    if (!a || !f || a->m < 1 || a->ncols < 1) return SPMM_HOST_ERR_ARG;
+    const int64_t m = a->m, n = a->ncols, nnz = a->nnz;
+    const int32_t *rp = a->row_ptr, *ci = a->col_idx;
+    double s_deg = 0, s_deg2 = 0, s_bw = 0, s_bw2 = 0, s_sc = 0, s_sc2 = 0, s_neigh = 0, s_sim = 0;
+    int64_t max_deg = 0, nonempty = 0;
+#pragma omp parallel for schedule(static) reduction(+ : s_deg, s_deg2, s_bw, s_bw2, s_sc, s_sc2, s_neigh, s_sim, \
+                                                        nonempty) reduction(max : max_deg)
+    for (int64_t i = 0; i < m; ++i) {
+        const int64_t js = rp[i], je = rp[i + 1], d = je - js;
+        s_deg += (double)d;
+        s_deg2 += (double)d * (double)d;
+        if (d > max_deg) max_deg = d;
+        if (d == 0) continue;
+        // bandwidth / scatter (csr_util_gen.c:296-309)
+        int64_t cmin = ci[js], cmax = ci[js];
+        for (int64_t j = js; j < je; ++j) {
+            cmin = std::min<int64_t>(cmin, ci[j]);
+            cmax = std::max<int64_t>(cmax, ci[j]);
+        }
+        const double b = (double)(cmax - cmin), sc = b > 0 ? (double)d / b : 0.0;
+        s_bw += b;
+        s_bw2 += b * b;
+        s_sc += sc;
+        s_sc2 += sc * sc;
+        // row neighbours, window 1 (csr_util_gen.c:459-490): pairs j<k with col[k]-col[j] <= 1, counted twice
+        for (int64_t j = js; j < je; ++j)
+            for (int64_t k = j + 1; k < je; ++k) {
+                if (ci[k] - ci[j] > 1) break;
+                s_neigh += 2.0;
+            }
+        // cross-row similarity, window 1 (csr_util_gen.c:553-610): next non-empty row
+        ++nonempty;
+        int64_t l = i + 1;
+        while (l < m && rp[l + 1] - rp[l] == 0) ++l;
+        if (l < m) {
+            int64_t k = rp[l];
+            const int64_t ke = rp[l + 1];
+            int64_t sim = 0;
+            for (int64_t j = js; j < je; ++j) {
+                while (k < ke) {
+                    const int64_t diff = (int64_t)ci[k] - ci[j];
+                    if (std::llabs(diff) <= 1) {
+                        ++sim;
+                        break;
+                    }
+                    if (diff <= 0)
+                        ++k;
+                    else
+                        break;
+                }
+            }
+            s_sim += (double)sim / (double)d;
+        }
+    }
+    memset(f, 0, sizeof(*f));
+    f->nr_rows = m;
+    f->nr_cols = n;
+    f->nr_nzeros = nnz;
+    f->density = (double)nnz / ((double)m * (double)n);
+    f->mem_footprint = ((double)nnz * 12.0 + (double)(m + 1) * 4.0) / (1024.0 * 1024.0);
+    const double mf = f->mem_footprint;
+    snprintf(f->mem_range, sizeof(f->mem_range), "%s",
+             mf < 4 ? "[0-4]" : mf < 32 ? "[4-32]" : mf < 512 ? "[32-512]" : mf < 2048 ? "[512-2048]" : "[2048-]");
+    const double dm = (double)m;
+    f->avg_nnz_per_row = s_deg / dm;
+    f->std_nnz_per_row = std::sqrt(std::max(0.0, s_deg2 / dm - f->avg_nnz_per_row * f->avg_nnz_per_row));
+    f->avg_bw = s_bw / dm;  // mean over all rows, empty rows count 0 (array_mean(bandwidths, m))
+    f->std_bw = std::sqrt(std::max(0.0, s_bw2 / dm - f->avg_bw * f->avg_bw));
+    f->avg_bw_scaled = f->avg_bw / (double)n;
+    f->std_bw_scaled = f->std_bw / (double)n;
+    f->avg_sc = s_sc / dm;
+    f->std_sc = std::sqrt(std::max(0.0, s_sc2 / dm - f->avg_sc * f->avg_sc));
+    f->avg_sc_scaled = f->avg_sc;  // scatter is already a ratio
+    f->std_sc_scaled = f->std_sc;
+    f->max_nnz_per_row = max_deg;
+    f->skew = f->avg_nnz_per_row > 0 ? ((double)max_deg - f->avg_nnz_per_row) / f->avg_nnz_per_row : 0.0;
+    f->avg_num_neighbours = nnz > 0 ? s_neigh / (double)nnz : 0.0;
+    f->cross_row_similarity = nonempty > 0 ? s_sim / (double)nonempty : 0.0;
+    return SPMM_HOST_OK;
+}
+
+void spmm_host_csr_free(spmm_csr_t *a) {
+    if (!a) return;
+    free(a->row_ptr);
+    free(a->col_idx);
+    free(a->values);
+    a->row_ptr = nullptr;
+    a->col_idx = nullptr;
+    a->values = nullptr;
+}
+
+void spmm_host_drand48_fill(int64_t seed, double *out, int64_t n) {
+    uint64_t X = (((uint64_t)seed) << 16) | 0x330EULL;
+    for (int64_t i = 0; i < n; ++i) {
+        X = (0x5DEECE66DULL * X + 0xBULL) & ((1ULL << 48) - 1);
+        out[i] = std::ldexp((double)X, -48);
+    }
+}
+
+void spmm_host_uniform_fill(int64_t seed, double lo, double hi, double *out, int64_t n) {
+    const int64_t CH = 1 << 16;
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < (n + CH - 1) / CH; ++c) {
+        Rng r((uint64_t)seed, (uint64_t)c, 99);
+        const int64_t e = std::min<int64_t>(n, (c + 1) * CH);
+        for (int64_t i = c * CH; i < e; ++i) out[i] = lo + (hi - lo) * r.uniform();
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,351 @@
+"""spmm_amd -- Python host mirror of the reference's SpMM plugin surface, over the engine's C ABI.
+
+The reference drives one kernel plugin per executable through ``csr_to_format(...)`` and ``MF->spmm(x, y, k)``
+(benchmark_code/CPU/AMD/spmv_code_bench/spmv_kernel.h:9-30, spmm_kernel_csr.cpp:21-66).  This module exposes
+the same surface on top of ``lib/libspmm_hip.so`` (include/spmm_hip.h) plus the host input path
+``lib/libspmm_host.so`` (include/spmm_host.h: .mtx reader, coo_to_csr, synthetic generator, features,
+CheckAccuracy).
+
+There is no CPU fallback: if the HIP library is missing this module raises at import, and every compute call goes
+to the GPU through the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parents[1]          # spmm-research_amd/
+LIB_DIR = PKG_ROOT / "lib"
+
+F64, F32 = 0, 1
+B_COL_MAJOR, B_ROW_MAJOR = 0, 1
+SEQ_MAX = 2048
+STATUS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP runtime error", -4: "no such HIP device",
+          -5: "k mismatch", -6: "malformed CSR", -7: "size overflow"}
+
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_i64 = C.c_int64
+
+
+class SpmmHipError(RuntimeError):
+    def __init__(self, where: str, status: int, detail: str = ""):
+        super().__init__(f"{where}: {STATUS.get(status, status)} ({status}) {detail}".rstrip())
+        self.status = status
+
+
+def _open(name: str) -> C.CDLL:
+    path = LIB_DIR / name
+    if not path.exists():
+        raise ImportError(f"{path} is not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build()); "
+                          "the engine has no CPU fallback")
+    return C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+
+
+class _CSRStruct(C.Structure):
+    _fields_ = [("m", _i64), ("ncols", _i64), ("nnz", _i64), ("row_ptr", C.POINTER(C.c_int32)),
+                ("col_idx", C.POINTER(C.c_int32)), ("values", C.POINTER(C.c_double))]
+
+
+class _GenParams(C.Structure):
+    _fields_ = [("nr_rows", _i64), ("nr_cols", _i64), ("avg_nnz_per_row", C.c_double),
+                ("std_nnz_per_row", C.c_double), ("distribution", C.c_char * 16), ("placement", C.c_char * 16),
+                ("bw", C.c_double), ("skew", C.c_double), ("avg_num_neighbours", C.c_double),
+                ("cross_row_similarity", C.c_double), ("seed", _i64)]
+
+
+class _Features(C.Structure):
+    _fields_ = [("distribution", C.c_char * 16), ("placement", C.c_char * 16), ("seed", _i64),
+                ("nr_rows", _i64), ("nr_cols", _i64), ("nr_nzeros", _i64), ("density", C.c_double),
+                ("mem_footprint", C.c_double), ("mem_range", C.c_char * 32),
+                ("avg_nnz_per_row", C.c_double), ("std_nnz_per_row", C.c_double),
+                ("avg_bw", C.c_double), ("std_bw", C.c_double), ("avg_bw_scaled", C.c_double),
+                ("std_bw_scaled", C.c_double), ("avg_sc", C.c_double), ("std_sc", C.c_double),
+                ("avg_sc_scaled", C.c_double), ("std_sc_scaled", C.c_double), ("skew", C.c_double),
+                ("avg_num_neighbours", C.c_double), ("cross_row_similarity", C.c_double),
+                ("max_nnz_per_row", _i64)]
+
+
+def _bind_hip(L: C.CDLL) -> C.CDLL:
+    vp, i32, i64 = C.c_void_p, C.c_int32, _i64
+    L.spmm_hip_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)]
+    L.spmm_hip_run.argtypes = [vp, vp, vp, i32]
+    L.spmm_hip_run_device.argtypes = [vp, vp, i32, vp, i32, vp]
+    L.spmm_hip_plan.argtypes = [vp, i32]
+    L.spmm_hip_last_times.argtypes = [vp, _f64p]
+    L.spmm_hip_stats_labels.argtypes = [C.c_char_p, C.c_long]
+    L.spmm_hip_stats.argtypes = [vp, C.c_char_p, C.c_long]
+    L.spmm_hip_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
+    L.spmm_hip_device_ptrs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+    L.spmm_hip_destroy.argtypes = [vp]
+    L.spmm_hip_partition_rows.argtypes = [_i32p, i64, i64, i64, i64, C.POINTER(i64), C.POINTER(i64)]
+    L.spmm_hip_bytes_alg.argtypes = [i64, i64, i64, i32, i32]
+    L.spmm_hip_bytes_alg.restype = C.c_double
+    L.spmm_hip_strerror.argtypes = [C.c_int]
+    L.spmm_hip_strerror.restype = C.c_char_p
+    L.spmm_hip_last_error_detail.restype = C.c_char_p
+    L.spmm_hip_device_count.argtypes = [C.POINTER(C.c_int)]
+    L.spmm_hip_version.restype = C.c_char_p
+    return L
+
+
+def _bind_host(L: C.CDLL) -> C.CDLL:
+    vp, i64 = C.c_void_p, _i64
+    L.spmm_host_parse_gen_line.argtypes = [C.c_char_p, C.POINTER(_GenParams)]
+    L.spmm_host_generate.argtypes = [C.POINTER(_GenParams), C.POINTER(_CSRStruct)]
+    L.spmm_host_generate_row_ptr.argtypes = [C.POINTER(_GenParams), _i32p]
+    L.spmm_host_generate_rows.argtypes = [C.POINTER(_GenParams), i64, i64, C.POINTER(_CSRStruct)]
+    L.spmm_host_features.argtypes = [C.POINTER(_CSRStruct), C.POINTER(_Features)]
+    L.spmm_host_mtx_read.argtypes = [C.c_char_p, C.POINTER(_CSRStruct), C.c_char_p, C.c_int, C.POINTER(C.c_int32)]
+    L.spmm_host_coo_to_csr.argtypes = [_i32p, _i32p, vp, i64, i64, _i32p, _i32p, _f64p]
+    L.spmm_host_csr_free.argtypes = [C.POINTER(_CSRStruct)]
+    L.spmm_host_drand48_fill.argtypes = [i64, _f64p, i64]
+    L.spmm_host_uniform_fill.argtypes = [i64, C.c_double, C.c_double, _f64p, i64]
+    L.spmm_host_check_accuracy.argtypes = [_i32p, _i32p, _f64p, i64, i64, _f64p, C.c_int32, vp, C.c_int32,
+                                           C.c_double, _f64p]
+    return L
+
+
+hip = _bind_hip(_open("libspmm_hip.so"))
+host = _bind_host(_open("libspmm_host.so"))
+
+def _detail() -> str:
+    d = hip.spmm_hip_last_error_detail()
+    return d.decode() if d else ""
+
+
+def _check(where: str, st: int):
+    if st != 0:
+        raise SpmmHipError(where, st, _detail())
+
+
+# ------------------------------------------------------------------------------------------------ host side
+@dataclass
+class CSR:
+    row_ptr: np.ndarray   # int32 [m+1]
+    col_idx: np.ndarray   # int32 [nnz]
+    values: np.ndarray    # float64 [nnz] (csr_a_ref)
+    m: int
+    ncols: int
+
+    @property
+    def nnz(self) -> int:
+        return int(self.row_ptr[-1]) if len(self.row_ptr) else 0
+
+
+def _take_csr(s: _CSRStruct) -> CSR:
+    m, n, nnz = s.m, s.ncols, s.nnz
+    rp = np.ctypeslib.as_array(s.row_ptr, (m + 1,)).copy()
+    ci = np.ctypeslib.as_array(s.col_idx, (max(nnz, 1),))[:nnz].copy()
+    va = np.ctypeslib.as_array(s.values, (max(nnz, 1),))[:nnz].copy()
+    host.spmm_host_csr_free(C.byref(s))
+    return CSR(rp, ci, va, m, n)
+
+
+def gen_params(line: str | None = None, **kw) -> _GenParams:
+    """Generator parameters from an 11-field line (the reference's argv order) and/or keywords."""
+    p = _GenParams()
+    if line is not None:
+        st = host.spmm_host_parse_gen_line(line.encode(), C.byref(p))
+        if st != 0:
+            raise ValueError(f"cannot parse generator line {line!r}")
+    for k, v in kw.items():
+        setattr(p, k, v.encode() if isinstance(v, str) else v)
+    return p
+
+
+def generate(params: _GenParams) -> CSR:
+    s = _CSRStruct()
+    st = host.spmm_host_generate(C.byref(params), C.byref(s))
+    if st != 0:
+        raise RuntimeError(f"generator failed ({st})")
+    return _take_csr(s)
+
+
+def generate_row_ptr(params: _GenParams) -> np.ndarray:
+    rp = np.empty(params.nr_rows + 1, np.int32)
+    st = host.spmm_host_generate_row_ptr(C.byref(params), rp)
+    if st != 0:
+        raise RuntimeError(f"generator failed ({st})")
+    return rp
+
+
+def generate_rows(params: _GenParams, r0: int, r1: int) -> CSR:
+    s = _CSRStruct()
+    st = host.spmm_host_generate_rows(C.byref(params), r0, r1, C.byref(s))
+    if st != 0:
+        raise RuntimeError(f"generator failed ({st})")
+    return _take_csr(s)
+
+
+def features(a: CSR) -> dict:
+    s = _CSRStruct(a.m, a.ncols, a.nnz, a.row_ptr.ctypes.data_as(C.POINTER(C.c_int32)),
+                   a.col_idx.ctypes.data_as(C.POINTER(C.c_int32)), a.values.ctypes.data_as(C.POINTER(C.c_double)))
+    f = _Features()
+    st = host.spmm_host_features(C.byref(s), C.byref(f))
+    if st != 0:
+        raise RuntimeError(f"features failed ({st})")
+    out = {}
+    for name, _t in _Features._fields_:
+        v = getattr(f, name)
+        out[name] = v.decode() if isinstance(v, bytes) else v
+    return out
+
+
+def mtx_read(path: str | os.PathLike) -> tuple[CSR, str, int]:
+    """.mtx -> CSR with the indexing of the reference's mtx_read + coo_to_csr; returns (csr, field, symmetry)."""
+    s = _CSRStruct()
+    field = C.create_string_buffer(32)
+    sym = C.c_int32()
+    st = host.spmm_host_mtx_read(os.fsencode(str(path)), C.byref(s), field, 32, C.byref(sym))
+    if st != 0:
+        raise ValueError(f"cannot read {path} (status {st})")
+    return _take_csr(s), field.value.decode(), sym.value
+
+
+def coo_to_csr(R, Cc, V, m: int) -> CSR:
+    R = np.ascontiguousarray(R, np.int32)
+    Cc = np.ascontiguousarray(Cc, np.int32)
+    nnz = len(R)
+    rp = np.empty(m + 1, np.int32)
+    ci = np.empty(max(nnz, 1), np.int32)
+    va = np.empty(max(nnz, 1), np.float64)
+    vptr = None if V is None else np.ascontiguousarray(V, np.float64).ctypes.data_as(C.c_void_p)
+    st = host.spmm_host_coo_to_csr(R, Cc, vptr, m, nnz, rp, ci, va)
+    if st != 0:
+        raise ValueError(f"coo_to_csr failed ({st})")
+    ncols = int(Cc.max()) + 1 if nnz else 0
+    return CSR(rp, ci[:nnz], va[:nnz], m, ncols)
+
+
+def drand48(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, np.float64)
+    host.spmm_host_drand48_fill(seed, out, n)
+    return out
+
+
+def uniform(seed: int, lo: float, hi: float, n: int) -> np.ndarray:
+    out = np.empty(n, np.float64)
+    host.spmm_host_uniform_fill(seed, lo, hi, out, n)
+    return out
+
+
+def check_accuracy(a: CSR, x_ref_colmajor: np.ndarray, k: int, y_test: np.ndarray, eps: float) -> np.ndarray:
+    """Harness CheckAccuracy (spmv_bench.cpp:121-206) + normwise check; see include/spmm_host.h for out[]."""
+    out = np.empty(11, np.float64)
+    y = np.ascontiguousarray(y_test)
+    dt = 1 if y.dtype == np.float32 else 0
+    host.spmm_host_check_accuracy(a.row_ptr, a.col_idx, np.ascontiguousarray(a.values, np.float64), a.m, a.ncols,
+                                  np.ascontiguousarray(x_ref_colmajor, np.float64), k, y.ctypes.data_as(C.c_void_p),
+                                  dt, eps, out)
+    return out
+
+
+def partition_rows(row_ptr: np.ndarray, nnz: int, workers: int, pos: int) -> tuple[int, int]:
+    """loop_partitioner_balance_prefix_sums (lib/parallel_util.h:141-165): rows [s, e) of worker pos."""
+    s, e = _i64(), _i64()
+    _check("partition_rows", hip.spmm_hip_partition_rows(np.ascontiguousarray(row_ptr, np.int32),
+                                                           len(row_ptr) - 1, nnz, workers, pos,
+                                                           C.byref(s), C.byref(e)))
+    return s.value, e.value
+
+
+def bytes_alg(m: int, ncols: int, nnz: int, k: int, dtype: int = F64) -> float:
+    return hip.spmm_hip_bytes_alg(m, ncols, nnz, k, dtype)
+
+
+def device_count() -> int:
+    n = C.c_int()
+    hip.spmm_hip_device_count(C.byref(n))
+    return n.value
+
+
+def stats_labels() -> str:
+    buf = C.create_string_buffer(4096)
+    w = hip.spmm_hip_stats_labels(buf, 4096)
+    return buf.value[:max(w, 0)].decode()
+
+
+# ------------------------------------------------------------------------------------------- plugin mirror
+class MatrixFormat:
+    """Mirror of ``struct Matrix_Format`` (spmv_kernel.h:9-26) backed by an engine handle on one GPU."""
+
+    format_name = "HIP_CSR_MI355X"
+
+    def __init__(self, row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0):
+        self.m, self.n, self.nnz = int(m), int(n), int(nnz)
+        vals = np.ascontiguousarray(values)
+        if vals.dtype not in (np.float64, np.float32):
+            raise TypeError("values must be float64 or float32 (ValueType)")
+        self.dtype = np.dtype(vals.dtype)
+        self._dt = F64 if self.dtype == np.float64 else F32
+        rp = np.ascontiguousarray(row_ptr, np.int32)
+        ci = np.ascontiguousarray(col_ind, np.int32)
+        if len(ci) == 0:
+            ci = np.zeros(1, np.int32)
+            vals = np.zeros(1, self.dtype)
+        self._h = C.c_void_p()
+        _check("csr_to_format", hip.spmm_hip_create(rp, ci, vals.ctypes.data_as(C.c_void_p), self.m, self.n,
+                                                    self.nnz, int(k), self._dt, int(device), C.byref(self._h)))
+        self.csr_mem_footprint = self.nnz * (self.dtype.itemsize + 4) + (self.m + 1) * 4
+        self.mem_footprint = float(self.info()[7])
+
+    # Matrix_Format::spmm(x, y, k): host x column-major [k][n], host y row-major [m][k] (overwritten)
+    def spmm(self, x: np.ndarray, y: np.ndarray, k: int) -> None:
+        if x.dtype != self.dtype or y.dtype != self.dtype:
+            raise TypeError("x and y must have the handle's ValueType")
+        if x.size < self.n * k or y.size < self.m * k or not (x.flags.c_contiguous and y.flags.c_contiguous):
+            raise ValueError("x must hold n*k and y m*k contiguous values")
+        _check("spmm", hip.spmm_hip_run(self._h, x.ctypes.data_as(C.c_void_p), y.ctypes.data_as(C.c_void_p), k))
+
+    def spmm_device(self, d_b: int, b_layout: int, d_c: int, k: int, stream: int = 0) -> None:
+        """HBM-resident run: d_b / d_c are device addresses (e.g. torch tensor .data_ptr())."""
+        _check("spmm_device", hip.spmm_hip_run_device(self._h, C.c_void_p(d_b), b_layout, C.c_void_p(d_c), k,
+                                                      C.c_void_p(stream)))
+
+    def plan(self, k: int) -> None:
+        _check("plan", hip.spmm_hip_plan(self._h, k))
+
+    def last_times(self) -> dict:
+        t = np.zeros(4, np.float64)
+        _check("last_times", hip.spmm_hip_last_times(self._h, t))
+        return {"kernel_ms": t[0], "transpose_ms": t[1], "h2d_ms": t[2], "d2h_ms": t[3]}
+
+    def info(self) -> np.ndarray:
+        out = np.zeros(8, np.int64)
+        _check("info", hip.spmm_hip_info(self._h, out))
+        return out
+
+    def statistics_start(self) -> None:
+        pass
+
+    def statistics_print_data(self) -> str:
+        buf = C.create_string_buffer(4096)
+        w = hip.spmm_hip_stats(self._h, buf, 4096)
+        if w < 0:
+            raise SpmmHipError("stats", w, _detail())
+        return buf.value.decode()
+
+    def close(self) -> None:
+        if self._h:
+            hip.spmm_hip_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def csr_to_format(row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0) -> MatrixFormat:
+    """Factory with the reference's signature (spmv_kernel.h:29)."""
+    return MatrixFormat(row_ptr, col_ind, values, m, n, nnz, k, device)
+
+
+def statistics_print_labels() -> str:
+    return stats_labels()
