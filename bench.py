@@ -107,16 +107,11 @@ def main():
     npdtype = np.float64 if args.dtype == "f64" else np.float32
 
     # ---- global matrix: N stacked copies of the per-GPU shape, nnz-balanced row split (a8 partitioner)
-    p1 = S.gen_params(args.gen)
-    p = S.gen_params(args.gen)
-    p.nr_rows = p1.nr_rows * N
-    p.nr_cols = p1.nr_cols * N
-    p.bw = p1.bw / N
+    from spmm_amd import sharding
     t0 = time.perf_counter()
-    rp_global = S.generate_row_ptr(p)
-    nnz_global = int(rp_global[-1])
-    r0, r1 = S.partition_rows(rp_global, nnz_global, N, rank)
-    A = S.generate_rows(p, r0, r1)
+    p = sharding.weak_scaled_params(args.gen, N)
+    sh = sharding.make_shard(p, N, rank)
+    A = sh.a
     t_gen = time.perf_counter() - t0
 
     mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdtype), A.m, p.nr_cols, A.nnz, K, local_rank)
@@ -130,7 +125,7 @@ def main():
     if dist is not None:
         torch.cuda.synchronize()
         tb = time.perf_counter()
-        dist.broadcast(B, src=0)
+        sharding.broadcast_b(dist, B)        # RCCL over xGMI, once at setup
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - tb
     C = torch.empty((max(A.m, 1), K), device=dev, dtype=tdtype)

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/spmm_hip.h"
@@ -35,6 +36,23 @@ int fail(int status, const std::string &what) {
             return fail(SPMM_HIP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));            \
     } while (0)
 
+// Production kernel variant (chosen by tools/tune_kernel.py on MI355X; see DESIGN.md "Kernel tuning").
+#ifndef DEF_U
+#define DEF_U 16
+#endif
+#ifndef DEF_CAP
+#define DEF_CAP 2048
+#endif
+#ifndef DEF_NTC
+#define DEF_NTC 1
+#endif
+#ifndef DEF_REMAP
+#define DEF_REMAP 0
+#endif
+#ifndef DEF_IL
+#define DEF_IL 1
+#endif
+
 struct Plan {
     int k = -1;
     int vec = 1;   // values per lane per load (16 B where K allows)
@@ -54,7 +72,10 @@ struct spmm_hip_handle {
     int32_t *d_col = nullptr;
     void *d_val = nullptr;
 
-    // inspector output
+    // inspector output (block capacity = the kernel variant's CAP)
+    int cap = 2048;
+    int variant[5] = {DEF_U, DEF_CAP, DEF_NTC, DEF_REMAP, DEF_IL};
+    std::vector<int32_t> h_row_ptr_copy;  // kept only by the tuning build (re-blocking for another CAP)
     int nblk = 0;
     int32_t *d_blk_rows = nullptr;
     int nchunks = 0, nlong = 0;
@@ -101,14 +122,8 @@ Plan make_plan(int k, size_t vsize) {
     return p;
 }
 
-template <typename T>
-int launch_long(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s);
-
 template <typename T, int VEC, int G>
-void launch_rows_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
-    if (h->nblk > 0)
-        spmm_rows_kernel<T, VEC, G, 4><<<h->nblk, WG, 0, s>>>(h->d_row_ptr, h->d_col, (const T *)h->d_val,
-                                                              h->d_blk_rows, h->nblk, B, C, K);
+void launch_long_path(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     if (h->nchunks > 0) {
         spmm_long_chunks_kernel<T, VEC, G>
             <<<h->nchunks, WG, 0, s>>>(h->d_col, (const T *)h->d_val, h->d_chunks, B, (T *)h->d_part, K);
@@ -116,6 +131,43 @@ void launch_rows_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         spmm_long_combine_kernel<T>
             <<<(unsigned)((tot + WG - 1) / WG), WG, 0, s>>>(h->d_long_rows, h->nlong, (const T *)h->d_part, C, K);
     }
+}
+
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL>
+void launch_rows_v(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
+    if (h->nblk > 0)
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, IL>
+            <<<h->nblk, WG, 0, s>>>(h->d_row_ptr, h->d_col, (const T *)h->d_val, h->d_blk_rows, h->nblk, B, C, K);
+    launch_long_path<T, VEC, G>(h, B, C, K, s);
+}
+
+#ifdef SPMM_TUNING
+// Tuning build only: the K=32 fp64 shape (VEC=2, G=16) over a grid of variants, selected at run time.
+template <int U, int CAP, bool NTC, bool REMAP, int IL>
+bool try_variant(spmm_hip_t *h, const double *B, double *C, int K, hipStream_t s) {
+    const int *v = h->variant;
+    if (v[0] != U || v[1] != CAP || v[2] != (int)NTC || v[3] != (int)REMAP || v[4] != IL) return false;
+    launch_rows_v<double, 2, 16, U, CAP, NTC, REMAP, IL>(h, B, C, K, s);
+    return true;
+}
+#define TV(U, CAP, NTC, REMAP, IL) try_variant<U, CAP, NTC, REMAP, IL>(h, B, C, K, s) ||
+#define TV_CAP(U, CAP) TV(U, CAP, false, false, 1) TV(U, CAP, false, true, 1) TV(U, CAP, true, false, 1) \
+    TV(U, CAP, true, true, 1) TV(U, CAP, true, true, 2) TV(U, CAP, false, true, 2)
+bool launch_tuned(spmm_hip_t *h, const double *B, double *C, int K, hipStream_t s) {
+    return TV_CAP(4, 1024) TV_CAP(4, 2048) TV_CAP(8, 1024) TV_CAP(8, 2048) TV_CAP(2, 2048)
+        TV(12, 2048, true, false, 1) TV(16, 2048, true, false, 1) TV(8, 4096, true, false, 1)
+        TV(16, 4096, true, false, 1) TV(6, 2048, true, false, 1) TV(4, 2048, true, false, 2) false;
+}
+#endif
+
+template <typename T, int VEC, int G>
+void launch_rows_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
+#ifdef SPMM_TUNING
+    if constexpr (std::is_same<T, double>::value && VEC == 2 && G == 16) {
+        if (launch_tuned(h, B, C, K, s)) return;
+    }
+#endif
+    launch_rows_v<T, VEC, G, DEF_U, DEF_CAP, (bool)DEF_NTC, (bool)DEF_REMAP, DEF_IL>(h, B, C, K, s);
 }
 
 template <typename T, int VEC>
@@ -173,9 +225,9 @@ void free_k_buffers(spmm_hip_t *h) {
     h->last_x = nullptr;
 }
 
-// Inspector: greedy nnz-balanced row blocks (<= CAP_NNZ nonzeros, <= CAP_ROWS rows; a longer row is a block of
-// its own and is cut into CAP_NNZ chunks for the long path).
-void build_blocks(const int32_t *rp, int64_t m, std::vector<int32_t> &blk, std::vector<int4> &chunks,
+// Inspector: greedy nnz-balanced row blocks (<= cap nonzeros, <= CAP_ROWS rows; a longer row is a block of
+// its own and is cut into CAP_LONG chunks for the long path).
+void build_blocks(const int32_t *rp, int64_t m, int cap, std::vector<int32_t> &blk, std::vector<int4> &chunks,
                   std::vector<int4> &long_rows) {
     blk.clear();
     chunks.clear();
@@ -184,13 +236,13 @@ void build_blocks(const int32_t *rp, int64_t m, std::vector<int32_t> &blk, std::
     int64_t r = 0;
     while (r < m) {
         const int64_t len = (int64_t)rp[r + 1] - rp[r];
-        if (len > CAP_NNZ) {
+        if (len > cap) {
             if (blk.back() != r) blk.push_back((int32_t)r);
-            const int nslot = (int)((len + CAP_NNZ - 1) / CAP_NNZ);
+            const int nslot = (int)((len + CAP_LONG - 1) / CAP_LONG);
             long_rows.push_back(make_int4((int)r, (int)chunks.size(), nslot, 0));
             for (int q = 0; q < nslot; ++q) {
-                const int a = rp[r] + q * CAP_NNZ;
-                const int e = (int)std::min<int64_t>((int64_t)a + CAP_NNZ, rp[r + 1]);
+                const int a = rp[r] + q * CAP_LONG;
+                const int e = (int)std::min<int64_t>((int64_t)a + CAP_LONG, rp[r + 1]);
                 chunks.push_back(make_int4((int)r, a, e, (int)chunks.size()));
             }
             blk.push_back((int32_t)(r + 1));
@@ -199,7 +251,7 @@ void build_blocks(const int32_t *rp, int64_t m, std::vector<int32_t> &blk, std::
         }
         int64_t start = blk.back();
         int64_t nnz_blk = (int64_t)rp[r] - rp[start];
-        if (r - start >= CAP_ROWS || nnz_blk + len > CAP_NNZ) {
+        if (r - start >= CAP_ROWS || nnz_blk + len > cap) {
             blk.push_back((int32_t)r);
             continue;
         }
@@ -308,7 +360,11 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
 
     std::vector<int32_t> blk;
     std::vector<int4> long_rows;
-    build_blocks(row_ptr, m, blk, h->h_chunks, long_rows);
+    h->cap = DEF_CAP;
+    build_blocks(row_ptr, m, h->cap, blk, h->h_chunks, long_rows);
+#ifdef SPMM_TUNING
+    h->h_row_ptr_copy.assign(row_ptr, row_ptr + m + 1);
+#endif
     h->nblk = (int)blk.size() - 1;
     h->nchunks = (int)h->h_chunks.size();
     h->nlong = (int)long_rows.size();
@@ -525,5 +581,46 @@ int spmm_hip_destroy(spmm_hip_t *h) {
     delete h;
     return SPMM_HIP_OK;
 }
+
+#ifdef SPMM_TUNING
+// Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): pick the K=32 fp64 row-kernel variant and
+// rebuild the row-block table for its capacity.
+int spmm_hip_tune_select(spmm_hip_t *h, int u, int cap, int ntc, int remap, int il) {
+    if (!h || h->h_row_ptr_copy.empty()) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<int32_t> blk;
+    std::vector<int4> long_rows;
+    build_blocks(h->h_row_ptr_copy.data(), h->m, cap, blk, h->h_chunks, long_rows);
+    if (h->d_blk_rows) (void)hipFree(h->d_blk_rows);
+    if (h->d_chunks) (void)hipFree(h->d_chunks);
+    if (h->d_long_rows) (void)hipFree(h->d_long_rows);
+    h->d_blk_rows = nullptr;
+    h->d_chunks = nullptr;
+    h->d_long_rows = nullptr;
+    h->nblk = (int)blk.size() - 1;
+    h->nchunks = (int)h->h_chunks.size();
+    h->nlong = (int)long_rows.size();
+    HIPCHK(hipMalloc(&h->d_blk_rows, blk.size() * 4));
+    HIPCHK(hipMemcpy(h->d_blk_rows, blk.data(), blk.size() * 4, hipMemcpyHostToDevice));
+    if (h->nchunks > 0) {
+        HIPCHK(hipMalloc(&h->d_chunks, h->nchunks * sizeof(int4)));
+        HIPCHK(hipMalloc(&h->d_long_rows, h->nlong * sizeof(int4)));
+        HIPCHK(hipMemcpy(h->d_chunks, h->h_chunks.data(), h->nchunks * sizeof(int4), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(h->d_long_rows, long_rows.data(), h->nlong * sizeof(int4), hipMemcpyHostToDevice));
+        if (h->plan.k > 0) {
+            if (h->d_part) (void)hipFree(h->d_part);
+            HIPCHK(hipMalloc(&h->d_part, (size_t)h->nchunks * h->plan.k * h->vsize));
+        }
+    }
+    h->cap = cap;
+    h->variant[0] = u;
+    h->variant[1] = cap;
+    h->variant[2] = ntc;
+    h->variant[3] = remap;
+    h->variant[4] = il;
+    return SPMM_HIP_OK;
+}
+#endif
 
 }  // extern "C"

@@ -4,15 +4,17 @@
 // (benchmark_code/CPU/AMD/spmv_code_bench/spmm_kernel_csr.cpp:70-96):
 //     C[i][n] = sum_{j in row i} a[j] * B[ja[j]][n]      (left-to-right, from 0)
 // re-designed for MI355X:
-//   * one workgroup (256 lanes = 4 wave64) per nnz-balanced ROW BLOCK (<= CAP_NNZ nonzeros, <= CAP_ROWS rows),
+//   * one workgroup (256 lanes = 4 wave64) per nnz-balanced ROW BLOCK (<= CAP nonzeros, <= CAP_ROWS rows),
 //     consecutive row blocks dealt to the same XCD (L2 reuse of B rows shared by neighbouring rows);
-//   * the block's col_idx / values are streamed from HBM once, coalesced, into LDS;
+//   * the block's col_idx / values are streamed from HBM once, coalesced and non-temporal, into LDS;
 //   * a "row group" of G lanes owns one row: each lane owns VEC consecutive columns of K (16-byte loads of the
 //     row-major B row), walks the row's nonzeros in CSR order and accumulates with one FMA per nonzero --
 //     the same left-to-right fused chain as the reference built with its own flags, so results are bit-equal;
-//   * 256/G row groups per workgroup, 64/G per wavefront.
-// Rows longer than CAP_NNZ are split into chunks (spmm_long_chunks_kernel) whose partial sums are combined in
-// a fixed order (spmm_long_combine_kernel): deterministic, no atomics.
+//     U gathers are issued before their FMAs (memory-level parallelism), optionally for IL rows at once;
+//   * 256/G row groups per workgroup, 64/G per wavefront; C rows written with (optionally non-temporal)
+//     16-byte stores so the streamed output does not evict B from L2 / the Infinity Cache.
+// Rows longer than CAP are split into chunks (spmm_long_chunks_kernel) whose partial sums are combined in a
+// fixed order (spmm_long_combine_kernel): deterministic, no atomics.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,8 +22,8 @@
 namespace spmm {
 
 constexpr int WG = 256;          // lanes per workgroup (4 wavefronts)
-constexpr int CAP_NNZ = 2048;    // nonzeros staged per row block (also the longest row kept sequential)
 constexpr int CAP_ROWS = 512;    // rows per row block
+constexpr int CAP_LONG = 2048;   // nonzeros per long-row chunk
 constexpr int NXCD = 8;          // MI355X: 8 accelerator dies, one L2 each
 
 template <typename T, int N>
@@ -46,6 +48,16 @@ __device__ __forceinline__ void vfma(vec<T, N> &acc, T a, const vec<T, N> &b) {
     for (int i = 0; i < N; ++i) acc.v[i] = fma_(a, b.v[i], acc.v[i]);
 }
 
+template <typename T, int N, bool NT>
+__device__ __forceinline__ void vstore(T *p, const vec<T, N> &v) {
+    if constexpr (NT) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) __builtin_nontemporal_store(v.v[i], p + i);
+    } else {
+        *reinterpret_cast<vec<T, N> *>(p) = v;
+    }
+}
+
 // Bijective XCD-aware remap: hardware deals workgroups round-robin over the 8 XCDs (bid % 8 share one), so
 // give each XCD a contiguous run of row blocks.  Speed only; any placement gives the same result.
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
@@ -54,29 +66,93 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     return x * q + (x < r ? x : r) + i;
 }
 
+// One row, nonzeros [a, e) of the LDS-staged block: U gathers in flight, then U FMAs in CSR order.
+template <typename T, int VEC, int U>
+__device__ __forceinline__ vec<T, VEC> row_dot(const int32_t *s_col, const T *s_val, int a, int e,
+                                               const T *__restrict__ Bk, int K) {
+    using V = vec<T, VEC>;
+    V acc = vzero<T, VEC>();
+    int j = a;
+    for (; j + U <= e; j += U) {
+        V bv[U];
+        T av[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            av[u] = s_val[j + u];
+            bv[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[j + u] * K);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) vfma(acc, av[u], bv[u]);
+    }
+    if (j < e) {  // tail: predicated gathers, FMAs only for real nonzeros (keeps -0.0 sums bit-exact)
+        V bv[U];
+        T av[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (j + u < e) {
+                av[u] = s_val[j + u];
+                bv[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[j + u] * K);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u < e) vfma(acc, av[u], bv[u]);
+    }
+    return acc;
+}
+
+// Two rows at once: their gathers interleave (2U in flight), each row still summed in its own CSR order.
+template <typename T, int VEC, int U>
+__device__ __forceinline__ void row_dot2(const int32_t *s_col, const T *s_val, int a0, int e0, int a1, int e1,
+                                         const T *__restrict__ Bk, int K, vec<T, VEC> &acc0, vec<T, VEC> &acc1) {
+    using V = vec<T, VEC>;
+    acc0 = vzero<T, VEC>();
+    acc1 = vzero<T, VEC>();
+    const int n = max(e0 - a0, e1 - a1);
+    for (int t = 0; t < n; t += U) {
+        V b0[U], b1[U];
+        T v0[U], v1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (a0 + t + u < e0) {
+                v0[u] = s_val[a0 + t + u];
+                b0[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[a0 + t + u] * K);
+            }
+            if (a1 + t + u < e1) {
+                v1[u] = s_val[a1 + t + u];
+                b1[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[a1 + t + u] * K);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (a0 + t + u < e0) vfma(acc0, v0[u], b0[u]);
+            if (a1 + t + u < e1) vfma(acc1, v1[u], b1[u]);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ row blocks
-// blk_rows[b] .. blk_rows[b+1]: the rows of block b (every row of the block has <= CAP_NNZ nonzeros and the block
-// holds <= CAP_NNZ nonzeros; rows longer than CAP_NNZ form blocks of their own that this kernel skips: the long
-// path writes them).
-template <typename T, int VEC, int G, int UNROLL>
+// blk_rows[b] .. blk_rows[b+1]: the rows of block b (every row has <= CAP nonzeros, the block <= CAP in all);
+// a row longer than CAP is a block of its own that this kernel skips (the long path writes it).
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL>
 __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict__ row_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
                                                        const int32_t *__restrict__ blk_rows, int nblk,
                                                        const T *__restrict__ B, T *__restrict__ C, int K) {
     __shared__ int32_t s_rp[CAP_ROWS + 1];
-    __shared__ int32_t s_col[CAP_NNZ];
-    __shared__ T s_val[CAP_NNZ];
+    __shared__ int32_t s_col[CAP];
+    __shared__ T s_val[CAP];
     using V = vec<T, VEC>;
     constexpr int NG = WG / G;
 
-    const int b = xcd_remap(blockIdx.x, nblk);
+    const int b = REMAP ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
     const int tid = threadIdx.x;
     const int r0 = blk_rows[b], r1 = blk_rows[b + 1];
     const int nrows = r1 - r0;
     const int j0 = row_ptr[r0];
     const int nnz = row_ptr[r1] - j0;
-    if (nnz > CAP_NNZ) return;  // a long row: written by the long path
+    if (nnz > CAP) return;  // a long row: written by the long path
 
     for (int i = tid; i <= nrows; i += WG) s_rp[i] = row_ptr[r0 + i] - j0;
     for (int i = tid; i < nnz; i += WG) {
@@ -89,31 +165,22 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     const int grp = tid / G;
     for (int kc = 0; kc < K; kc += G * VEC) {
         const int kk = kc + lane * VEC;
-        const bool active = kk < K;
+        if (kk >= K) continue;
         const T *__restrict__ Bk = B + kk;
-        for (int r = grp; r < nrows; r += NG) {
-            const int a = s_rp[r], e = s_rp[r + 1];
-            V acc = vzero<T, VEC>();
-            if (active) {
-                int j = a;
-                for (; j + UNROLL <= e; j += UNROLL) {
-                    V bv[UNROLL];
-                    T av[UNROLL];
-#pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) {
-                        const int c = s_col[j + u];
-                        av[u] = s_val[j + u];
-                        bv[u] = *reinterpret_cast<const V *>(Bk + (size_t)c * K);
-                    }
-#pragma unroll
-                    for (int u = 0; u < UNROLL; ++u) vfma(acc, av[u], bv[u]);
-                }
-                for (; j < e; ++j) {
-                    const int c = s_col[j];
-                    const V bv = *reinterpret_cast<const V *>(Bk + (size_t)c * K);
-                    vfma(acc, s_val[j], bv);
-                }
-                *reinterpret_cast<V *>(C + (size_t)(r0 + r) * K + kk) = acc;
+        if constexpr (IL == 1) {
+            for (int r = grp; r < nrows; r += NG) {
+                const V acc = row_dot<T, VEC, U>(s_col, s_val, s_rp[r], s_rp[r + 1], Bk, K);
+                vstore<T, VEC, NTC>(C + (size_t)(r0 + r) * K + kk, acc);
+            }
+        } else {
+            for (int r = grp; r < nrows; r += 2 * NG) {
+                const int r2 = r + NG;
+                const bool has2 = r2 < nrows;
+                V acc0, acc1;
+                row_dot2<T, VEC, U>(s_col, s_val, s_rp[r], s_rp[r + 1], has2 ? s_rp[r2] : 0, has2 ? s_rp[r2 + 1] : 0,
+                                    Bk, K, acc0, acc1);
+                vstore<T, VEC, NTC>(C + (size_t)(r0 + r) * K + kk, acc0);
+                if (has2) vstore<T, VEC, NTC>(C + (size_t)(r0 + r2) * K + kk, acc1);
             }
         }
     }

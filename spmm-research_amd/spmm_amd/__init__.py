@@ -38,12 +38,27 @@ class SpmmHipError(RuntimeError):
         self.status = status
 
 
+def _preload_hip_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm bundles its own libamdhip64 (DT_NEEDED "libamdhip64.so", found
+    through its RPATH) while libspmm_hip.so needs "libamdhip64.so.7"; if the engine were loaded first the process
+    would end up with two runtimes.  Preloading torch's copy (soname libamdhip64.so.7) makes both resolve to it.
+    Set SPMM_HIP_RUNTIME=system to keep the system ROCm runtime instead."""
+    if os.environ.get("SPMM_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec and spec.origin:
+        rt = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+        if rt.exists():
+            C.CDLL(str(rt), mode=C.RTLD_GLOBAL)
+
+
 def _open(name: str) -> C.CDLL:
     path = LIB_DIR / name
     if not path.exists():
         raise ImportError(f"{path} is not built: run `make -C {PKG_ROOT}` (or __graft_entry__.build()); "
                           "the engine has no CPU fallback")
-    return C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+    return C.CDLL(str(path))
 
 
 class _CSRStruct(C.Structure):
@@ -110,6 +125,7 @@ def _bind_host(L: C.CDLL) -> C.CDLL:
     return L
 
 
+_preload_hip_runtime()
 hip = _bind_hip(_open("libspmm_hip.so"))
 host = _bind_host(_open("libspmm_host.so"))
 

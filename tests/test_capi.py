@@ -2,6 +2,7 @@
 import ctypes
 import re
 import subprocess
+import sys
 from pathlib import Path
 
 import pytest
@@ -33,10 +34,8 @@ def test_host_only_entry_points_without_gpu():
     import spmm_amd as S
     assert S.hip.spmm_hip_strerror(-6) == b"malformed CSR"
     assert S.stats_labels().startswith(",kernel_ms")
-    # the gfx950 code object is embedded
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(LIB / "libspmm_hip.so")],
-                         capture_output=True, text=True)
-    assert "gfx950" in (out.stdout + out.stderr)
+    # the gfx950 code object is embedded (offload bundle id)
+    assert b"amdgcn-amd-amdhsa--gfx950" in (LIB / "libspmm_hip.so").read_bytes()
 
 
 def test_harness_prints_reference_labels():
@@ -49,3 +48,13 @@ def test_harness_prints_reference_labels():
     assert "kernel_ms" in labels and "roofline_frac" in labels
     r = subprocess.run([str(exe)], capture_output=True, text=True, env={"USE_ARTIFICIAL_MATRICES": "1"})
     assert r.stderr.startswith("matrix_name,distribution,placement,seed,nr_rows")
+
+
+def test_single_hip_runtime_in_process():
+    """Importing the engine before torch must not leave two HIP runtimes mapped (spmm_amd preloads torch's)."""
+    code = ("import sys; sys.path.insert(0, 'spmm-research_amd'); import spmm_amd, torch; "
+            "maps = open('/proc/self/maps').read(); "
+            "print(len({l.split()[-1] for l in maps.splitlines() if 'libamdhip64' in l}))")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "1"

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""tools/collect_pmc.py -- HBM traffic and cache counters of the SpMM kernel, one rocprofv3 pass per counter group.
+
+Runs on the GPU box (via gpurun).  Each pass is `rocprofv3 --pmc <counters> -- python3 bench.py ...` with
+--kernel-trace-free PMC collection only (counters never share a run with sys/runtime traces).  Per-launch values are
+averaged over the dispatches of the dominant kernel (spmm_rows_kernel).
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads half
+the bytes of a wide coalesced streaming read, so the corrected read bytes are 2 * FETCH_SIZE * 1024.  Note both
+counters sit on the L2's memory side (TCC_EA0_*): Infinity-Cache hits are counted too, so this is L2-miss traffic
+(MALL + HBM), an upper bound on true HBM bytes.
+
+Writes profiles/pmc_<tag>.json (and profiles/pmc_latest.json) with the per-launch counters.
+"""
+import argparse
+import csv
+import json
+import shutil
+import subprocess
+import sys
+import time
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"], ["TCC_EA0_RDREQ_sum"],
+          ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"], ["TCP_TCC_READ_REQ_sum"]]
+KERNEL = "spmm_rows_kernel"
+
+
+def run_pass(i, counters, outdir, bench_args, timeout):
+    d = outdir / f"pass{i}"
+    if d.exists():
+        shutil.rmtree(d)
+    cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "pmc", "--",
+           sys.executable, str(ROOT / "bench.py"), *bench_args]
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    (outdir / f"pass{i}.log").write_text(r.stdout[-20000:] + "\n---stderr---\n" + r.stderr[-20000:])
+    if r.returncode != 0:
+        raise SystemExit(f"pass {i} {counters} failed rc={r.returncode} (see {outdir}/pass{i}.log)")
+    files = list(d.rglob("*counter_collection.csv"))
+    if not files:
+        raise SystemExit(f"pass {i}: no counter_collection.csv under {d}")
+    vals = defaultdict(lambda: defaultdict(float))
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if KERNEL not in row.get("Kernel_Name", ""):
+                continue
+            vals[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+    out = {}
+    for c, per in vals.items():
+        v = list(per.values())
+        out[c] = {"mean": sum(v) / len(v), "dispatches": len(v)}
+    print(f"pass {i} {counters}: {json.dumps(out)} ({time.time() - t0:.0f}s)", flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="latest")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--gen", default=None)
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--timeout", type=int, default=240)
+    args = ap.parse_args()
+    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--k", str(args.k)]
+    if args.gen:
+        bench_args += ["--gen", args.gen]
+    outdir = ROOT / "gpurun_out" / "pmc"
+    outdir.mkdir(parents=True, exist_ok=True)
+    res = {}
+    for i, counters in enumerate(PASSES):
+        res.update(run_pass(i, counters, outdir, bench_args, args.timeout))
+    sys.path.insert(0, str(ROOT))
+    import bench  # for the workload defaults only
+    gen = args.gen or bench.GEN_LINE
+    fetch_kib = res.get("FETCH_SIZE", {}).get("mean")
+    write_kib = res.get("WRITE_SIZE", {}).get("mean")
+    hbm = None
+    if fetch_kib is not None and write_kib is not None:
+        hbm = (2.0 * fetch_kib + write_kib) * 1024.0
+    summary = {"workload": gen, "k": args.k, "dtype": "f64", "kernel": KERNEL,
+               "counters_per_launch": {k: v["mean"] for k, v in res.items()},
+               "hbm_bytes_per_launch": hbm,
+               "hbm_bytes_note": "(2*FETCH_SIZE + WRITE_SIZE) KiB -> bytes; L2 memory-side, includes Infinity-Cache hits",
+               "raw_fetch_plus_write_bytes": None if hbm is None else (fetch_kib + write_kib) * 1024.0}
+    if "TCC_HIT_sum" in res and "TCC_MISS_sum" in res:
+        h, m = res["TCC_HIT_sum"]["mean"], res["TCC_MISS_sum"]["mean"]
+        summary["l2_hit_rate"] = h / (h + m) if h + m else None
+    prof = ROOT / "profiles"
+    prof.mkdir(exist_ok=True)
+    text = json.dumps(summary, indent=1)
+    (prof / f"pmc_{args.tag}.json").write_text(text)
+    (prof / "pmc_latest.json").write_text(text)
+    (ROOT / "gpurun_out" / f"pmc_{args.tag}.json").write_text(text)
+    print(text)
+
+
+if __name__ == "__main__":
+    main()
