@@ -52,6 +52,9 @@ int fail(int status, const std::string &what) {
 #ifndef DEF_IL
 #define DEF_IL 1
 #endif
+#ifndef DEF_BUF
+#define DEF_BUF 0
+#endif
 
 struct Plan {
     int k = -1;
@@ -74,7 +77,7 @@ struct spmm_hip_handle {
 
     // inspector output (block capacity = the kernel variant's CAP)
     int cap = 2048;
-    int variant[5] = {DEF_U, DEF_CAP, DEF_NTC, DEF_REMAP, DEF_IL};
+    int variant[6] = {DEF_U, DEF_CAP, DEF_NTC, DEF_REMAP, DEF_IL, DEF_BUF};
     std::vector<int32_t> h_row_ptr_copy;  // kept only by the tuning build (re-blocking for another CAP)
     int nblk = 0;
     int32_t *d_blk_rows = nullptr;
@@ -133,30 +136,38 @@ void launch_long_path(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     }
 }
 
-template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL>
+// 32-bit buffer offsets for the B gather are valid while B fits 4 GiB (else the flat 64-bit path is used).
+inline bool buf_ok(const spmm_hip_t *h) { return (uint64_t)h->ncols * (uint64_t)h->plan.k * h->vsize < (1ULL << 32); }
+
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL, bool BUF>
 void launch_rows_v(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
-    if (h->nblk > 0)
-        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, IL>
-            <<<h->nblk, WG, 0, s>>>(h->d_row_ptr, h->d_col, (const T *)h->d_val, h->d_blk_rows, h->nblk, B, C, K);
+    if (h->nblk > 0) {
+        const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * K * sizeof(T), 0xFFFFFFFFull);
+        if (BUF && !buf_ok(h))
+            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, IL, false><<<h->nblk, WG, 0, s>>>(
+                h->d_row_ptr, h->d_col, (const T *)h->d_val, h->d_blk_rows, h->nblk, B, C, K, bb);
+        else
+            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, IL, BUF><<<h->nblk, WG, 0, s>>>(
+                h->d_row_ptr, h->d_col, (const T *)h->d_val, h->d_blk_rows, h->nblk, B, C, K, bb);
+    }
     launch_long_path<T, VEC, G>(h, B, C, K, s);
 }
 
 #ifdef SPMM_TUNING
 // Tuning build only: the K=32 fp64 shape (VEC=2, G=16) over a grid of variants, selected at run time.
-template <int U, int CAP, bool NTC, bool REMAP, int IL>
+template <int U, int CAP, bool NTC, bool REMAP, int IL, bool BUF>
 bool try_variant(spmm_hip_t *h, const double *B, double *C, int K, hipStream_t s) {
     const int *v = h->variant;
-    if (v[0] != U || v[1] != CAP || v[2] != (int)NTC || v[3] != (int)REMAP || v[4] != IL) return false;
-    launch_rows_v<double, 2, 16, U, CAP, NTC, REMAP, IL>(h, B, C, K, s);
+    if (v[0] != U || v[1] != CAP || v[2] != (int)NTC || v[3] != (int)REMAP || v[4] != IL || v[5] != (int)BUF)
+        return false;
+    launch_rows_v<double, 2, 16, U, CAP, NTC, REMAP, IL, BUF>(h, B, C, K, s);
     return true;
 }
-#define TV(U, CAP, NTC, REMAP, IL) try_variant<U, CAP, NTC, REMAP, IL>(h, B, C, K, s) ||
-#define TV_CAP(U, CAP) TV(U, CAP, false, false, 1) TV(U, CAP, false, true, 1) TV(U, CAP, true, false, 1) \
-    TV(U, CAP, true, true, 1) TV(U, CAP, true, true, 2) TV(U, CAP, false, true, 2)
+#define TV(U, CAP, NTC, REMAP, IL, BUF) try_variant<U, CAP, NTC, REMAP, IL, BUF>(h, B, C, K, s) ||
 bool launch_tuned(spmm_hip_t *h, const double *B, double *C, int K, hipStream_t s) {
-    return TV_CAP(4, 1024) TV_CAP(4, 2048) TV_CAP(8, 1024) TV_CAP(8, 2048) TV_CAP(2, 2048)
-        TV(12, 2048, true, false, 1) TV(16, 2048, true, false, 1) TV(8, 4096, true, false, 1)
-        TV(16, 4096, true, false, 1) TV(6, 2048, true, false, 1) TV(4, 2048, true, false, 2) false;
+    return TV(8, 2048, true, false, 1, false) TV(16, 2048, true, false, 1, false) TV(16, 2048, true, false, 1, true)
+        TV(24, 2048, true, false, 1, true) TV(16, 1024, true, false, 1, true) TV(16, 2048, false, false, 1, true)
+        TV(16, 2048, true, true, 1, true) TV(8, 2048, true, false, 2, true) false;
 }
 #endif
 
@@ -167,7 +178,7 @@ void launch_rows_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         if (launch_tuned(h, B, C, K, s)) return;
     }
 #endif
-    launch_rows_v<T, VEC, G, DEF_U, DEF_CAP, (bool)DEF_NTC, (bool)DEF_REMAP, DEF_IL>(h, B, C, K, s);
+    launch_rows_v<T, VEC, G, DEF_U, DEF_CAP, (bool)DEF_NTC, (bool)DEF_REMAP, DEF_IL, (bool)DEF_BUF>(h, B, C, K, s);
 }
 
 template <typename T, int VEC>
@@ -383,13 +394,16 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
         }                                                                                                \
     } while (0)
 
-    const size_t rp_b = (size_t)(m + 1) * 4, col_b = (size_t)std::max<int64_t>(nnz, 1) * 4,
-                 val_b = (size_t)std::max<int64_t>(nnz, 1) * h->vsize, blk_b = blk.size() * 4;
+    // col / val are padded by 64 B: the kernel stages 16-byte vectors from a 16-byte boundary (spmm_rows_kernel)
+    const size_t rp_b = (size_t)(m + 1) * 4, col_b = (size_t)std::max<int64_t>(nnz, 1) * 4 + 64,
+                 val_b = (size_t)std::max<int64_t>(nnz, 1) * h->vsize + 64, blk_b = blk.size() * 4;
     HIPCHK_C(hipMalloc(&h->d_row_ptr, rp_b));
     HIPCHK_C(hipMalloc(&h->d_col, col_b));
     HIPCHK_C(hipMalloc(&h->d_val, val_b));
     HIPCHK_C(hipMalloc(&h->d_blk_rows, blk_b));
     HIPCHK_C(hipMemcpy(h->d_row_ptr, row_ptr, rp_b, hipMemcpyHostToDevice));
+    HIPCHK_C(hipMemset(h->d_col, 0, col_b));
+    HIPCHK_C(hipMemset(h->d_val, 0, val_b));
     if (nnz > 0) {
         HIPCHK_C(hipMemcpy(h->d_col, col_idx, (size_t)nnz * 4, hipMemcpyHostToDevice));
         HIPCHK_C(hipMemcpy(h->d_val, values, (size_t)nnz * h->vsize, hipMemcpyHostToDevice));
@@ -585,7 +599,7 @@ int spmm_hip_destroy(spmm_hip_t *h) {
 #ifdef SPMM_TUNING
 // Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): pick the K=32 fp64 row-kernel variant and
 // rebuild the row-block table for its capacity.
-int spmm_hip_tune_select(spmm_hip_t *h, int u, int cap, int ntc, int remap, int il) {
+int spmm_hip_tune_select(spmm_hip_t *h, int u, int cap, int ntc, int remap, int il, int buf) {
     if (!h || h->h_row_ptr_copy.empty()) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
@@ -619,6 +633,7 @@ int spmm_hip_tune_select(spmm_hip_t *h, int u, int cap, int ntc, int remap, int 
     h->variant[2] = ntc;
     h->variant[3] = remap;
     h->variant[4] = il;
+    h->variant[5] = buf;
     return SPMM_HIP_OK;
 }
 #endif

@@ -58,6 +58,40 @@ __device__ __forceinline__ void vstore(T *p, const vec<T, N> &v) {
     }
 }
 
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <typename T> struct stage_vec;
+template <> struct stage_vec<double> { using type = f64x2; static constexpr int n = 2; };
+template <> struct stage_vec<float> { using type = f32x4; static constexpr int n = 4; };
+
+// B row gather: 64-bit flat address, or a buffer load with a 32-bit byte offset from a wave-uniform resource
+// descriptor (fewer VGPRs per gather in flight; valid while ncols*K*sizeof(T) < 4 GiB, checked on the host).
+template <typename T, int VEC, bool BUF>
+struct BGather {
+    const T *__restrict__ base;  // B + kk
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t lane_off;           // kk * sizeof(T)
+    uint32_t row_bytes;          // K * sizeof(T)
+    int K;
+    __device__ __forceinline__ BGather(const T *B, int kk, int K_, uint32_t total_bytes) : K(K_) {
+        base = B + kk;
+        lane_off = (uint32_t)kk * sizeof(T);
+        row_bytes = (uint32_t)K_ * sizeof(T);
+        if constexpr (BUF) rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)B, (short)0, (int)total_bytes, 0x00020000);
+    }
+    __device__ __forceinline__ vec<T, VEC> operator()(int c) const {
+        if constexpr (BUF && VEC * sizeof(T) == 16) {
+            const i32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)c * row_bytes + lane_off, 0, 0);
+            vec<T, VEC> v;
+            __builtin_memcpy(&v, &r, 16);
+            return v;
+        } else {
+            return *reinterpret_cast<const vec<T, VEC> *>(base + (size_t)c * K);
+        }
+    }
+};
+
 // Bijective XCD-aware remap: hardware deals workgroups round-robin over the 8 XCDs (bid % 8 share one), so
 // give each XCD a contiguous run of row blocks.  Speed only; any placement gives the same result.
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
@@ -67,66 +101,50 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 }
 
 // One row, nonzeros [a, e) of the LDS-staged block: U gathers in flight, then U FMAs in CSR order.
-template <typename T, int VEC, int U>
+template <typename T, int VEC, int U, typename Gather>
 __device__ __forceinline__ vec<T, VEC> row_dot(const int32_t *s_col, const T *s_val, int a, int e,
-                                               const T *__restrict__ Bk, int K) {
+                                               const Gather &gather) {
     using V = vec<T, VEC>;
     V acc = vzero<T, VEC>();
     int j = a;
     for (; j + U <= e; j += U) {
         V bv[U];
-        T av[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            av[u] = s_val[j + u];
-            bv[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[j + u] * K);
-        }
+        for (int u = 0; u < U; ++u) bv[u] = gather(s_col[j + u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) vfma(acc, av[u], bv[u]);
+        for (int u = 0; u < U; ++u) vfma(acc, s_val[j + u], bv[u]);
     }
     if (j < e) {  // tail: predicated gathers, FMAs only for real nonzeros (keeps -0.0 sums bit-exact)
         V bv[U];
-        T av[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (j + u < e) {
-                av[u] = s_val[j + u];
-                bv[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[j + u] * K);
-            }
-        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (j + u < e) vfma(acc, av[u], bv[u]);
+            if (j + u < e) bv[u] = gather(s_col[j + u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u < e) vfma(acc, s_val[j + u], bv[u]);
     }
     return acc;
 }
 
 // Two rows at once: their gathers interleave (2U in flight), each row still summed in its own CSR order.
-template <typename T, int VEC, int U>
+template <typename T, int VEC, int U, typename Gather>
 __device__ __forceinline__ void row_dot2(const int32_t *s_col, const T *s_val, int a0, int e0, int a1, int e1,
-                                         const T *__restrict__ Bk, int K, vec<T, VEC> &acc0, vec<T, VEC> &acc1) {
+                                         const Gather &gather, vec<T, VEC> &acc0, vec<T, VEC> &acc1) {
     using V = vec<T, VEC>;
     acc0 = vzero<T, VEC>();
     acc1 = vzero<T, VEC>();
     const int n = max(e0 - a0, e1 - a1);
     for (int t = 0; t < n; t += U) {
         V b0[U], b1[U];
-        T v0[U], v1[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (a0 + t + u < e0) {
-                v0[u] = s_val[a0 + t + u];
-                b0[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[a0 + t + u] * K);
-            }
-            if (a1 + t + u < e1) {
-                v1[u] = s_val[a1 + t + u];
-                b1[u] = *reinterpret_cast<const V *>(Bk + (size_t)s_col[a1 + t + u] * K);
-            }
+            if (a0 + t + u < e0) b0[u] = gather(s_col[a0 + t + u]);
+            if (a1 + t + u < e1) b1[u] = gather(s_col[a1 + t + u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (a0 + t + u < e0) vfma(acc0, v0[u], b0[u]);
-            if (a1 + t + u < e1) vfma(acc1, v1[u], b1[u]);
+            if (a0 + t + u < e0) vfma(acc0, s_val[a0 + t + u], b0[u]);
+            if (a1 + t + u < e1) vfma(acc1, s_val[a1 + t + u], b1[u]);
         }
     }
 }
@@ -134,15 +152,19 @@ __device__ __forceinline__ void row_dot2(const int32_t *s_col, const T *s_val, i
 // ------------------------------------------------------------------------------------------------ row blocks
 // blk_rows[b] .. blk_rows[b+1]: the rows of block b (every row has <= CAP nonzeros, the block <= CAP in all);
 // a row longer than CAP is a block of its own that this kernel skips (the long path writes it).
-template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL>
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL, bool BUF>
 __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict__ row_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
                                                        const int32_t *__restrict__ blk_rows, int nblk,
-                                                       const T *__restrict__ B, T *__restrict__ C, int K) {
+                                                       const T *__restrict__ B, T *__restrict__ C, int K,
+                                                       uint32_t b_bytes) {
+    using SV = typename stage_vec<T>::type;
+    constexpr int SVN = stage_vec<T>::n;
+    constexpr int CAPP = CAP + 4;                         // staged window starts at a 16-byte boundary
     __shared__ int32_t s_rp[CAP_ROWS + 1];
-    __shared__ int32_t s_col[CAP];
-    __shared__ T s_val[CAP];
+    __shared__ __attribute__((aligned(16))) int32_t s_col[CAPP];
+    __shared__ __attribute__((aligned(16))) T s_val[CAPP];
     using V = vec<T, VEC>;
     constexpr int NG = WG / G;
 
@@ -151,13 +173,40 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     const int r0 = blk_rows[b], r1 = blk_rows[b + 1];
     const int nrows = r1 - r0;
     const int j0 = row_ptr[r0];
-    const int nnz = row_ptr[r1] - j0;
-    if (nnz > CAP) return;  // a long row: written by the long path
+    const int j1 = row_ptr[r1];
+    if (j1 - j0 > CAP) return;  // a long row: written by the long path
 
-    for (int i = tid; i <= nrows; i += WG) s_rp[i] = row_ptr[r0 + i] - j0;
-    for (int i = tid; i < nnz; i += WG) {
-        s_col[i] = __builtin_nontemporal_load(col_idx + j0 + i);
-        s_val[i] = __builtin_nontemporal_load(vals + j0 + i);
+    // Stage the block's col_idx / values: 16-byte non-temporal loads, ALL issued before the first wait (one
+    // memory round trip per block), from the 16-byte boundary jb <= j0 (arrays are padded on the device).
+    const int jb = j0 & ~3;
+    const int cnt = j1 - jb;
+    {
+        constexpr int NC = (CAPP / 4 + WG - 1) / WG;
+        constexpr int NV = (CAPP / SVN + WG - 1) / WG;
+        const int nc = (cnt + 3) / 4, nv = (cnt + SVN - 1) / SVN;
+        i32x4 cb[NC];
+        SV vb[NV];
+        int rp[(CAP_ROWS + 1 + WG - 1) / WG];
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+            if (tid + u * WG < nc)
+                cb[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(col_idx + jb) + tid + u * WG);
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+            if (tid + u * WG < nv)
+                vb[u] = __builtin_nontemporal_load(reinterpret_cast<const SV *>(vals + jb) + tid + u * WG);
+#pragma unroll
+        for (int u = 0; u < (CAP_ROWS + 1 + WG - 1) / WG; ++u)
+            if (tid + u * WG <= nrows) rp[u] = row_ptr[r0 + tid + u * WG];
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+            if (tid + u * WG < nc) reinterpret_cast<i32x4 *>(s_col)[tid + u * WG] = cb[u];
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+            if (tid + u * WG < nv) reinterpret_cast<SV *>(s_val)[tid + u * WG] = vb[u];
+#pragma unroll
+        for (int u = 0; u < (CAP_ROWS + 1 + WG - 1) / WG; ++u)
+            if (tid + u * WG <= nrows) s_rp[tid + u * WG] = rp[u] - jb;
     }
     __syncthreads();
 
@@ -166,10 +215,10 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     for (int kc = 0; kc < K; kc += G * VEC) {
         const int kk = kc + lane * VEC;
         if (kk >= K) continue;
-        const T *__restrict__ Bk = B + kk;
+        const BGather<T, VEC, BUF> gather(B, kk, K, b_bytes);
         if constexpr (IL == 1) {
             for (int r = grp; r < nrows; r += NG) {
-                const V acc = row_dot<T, VEC, U>(s_col, s_val, s_rp[r], s_rp[r + 1], Bk, K);
+                const V acc = row_dot<T, VEC, U>(s_col, s_val, s_rp[r], s_rp[r + 1], gather);
                 vstore<T, VEC, NTC>(C + (size_t)(r0 + r) * K + kk, acc);
             }
         } else {
@@ -178,7 +227,7 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
                 const bool has2 = r2 < nrows;
                 V acc0, acc1;
                 row_dot2<T, VEC, U>(s_col, s_val, s_rp[r], s_rp[r + 1], has2 ? s_rp[r2] : 0, has2 ? s_rp[r2 + 1] : 0,
-                                    Bk, K, acc0, acc1);
+                                    gather, acc0, acc1);
                 vstore<T, VEC, NTC>(C + (size_t)(r0 + r) * K + kk, acc0);
                 if (has2) vstore<T, VEC, NTC>(C + (size_t)(r0 + r2) * K + kk, acc1);
             }

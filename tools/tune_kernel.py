@@ -18,11 +18,9 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 
-VARIANTS = [(u, cap, ntc, remap, il)
-            for u, cap in ((4, 1024), (4, 2048), (8, 1024), (8, 2048), (2, 2048))
-            for ntc, remap, il in ((0, 0, 1), (0, 1, 1), (1, 0, 1), (1, 1, 1), (1, 1, 2), (0, 1, 2))] + \
-    [(12, 2048, 1, 0, 1), (16, 2048, 1, 0, 1), (8, 4096, 1, 0, 1), (16, 4096, 1, 0, 1), (6, 2048, 1, 0, 1),
-     (4, 2048, 1, 0, 2)]
+VARIANTS = [(8, 2048, 1, 0, 1, 0), (16, 2048, 1, 0, 1, 0), (16, 2048, 1, 0, 1, 1), (24, 2048, 1, 0, 1, 1),
+            (16, 1024, 1, 0, 1, 1), (16, 2048, 0, 0, 1, 1), (16, 2048, 1, 1, 1, 1), (8, 2048, 1, 0, 2, 1)]
+FIELDS = ("U", "CAP", "NTC", "REMAP", "IL", "BUF")
 
 
 def main():
@@ -37,7 +35,7 @@ def main():
     import torch
     import spmm_amd as S
     T = S._bind_hip(C.CDLL(str(ROOT / "spmm-research_amd" / "lib" / "libspmm_hip_tune.so")))
-    T.spmm_hip_tune_select.argtypes = [C.c_void_p] + [C.c_int] * 5
+    T.spmm_hip_tune_select.argtypes = [C.c_void_p] + [C.c_int] * 6
 
     A = S.generate(S.gen_params(args.gen))
     k = args.k
@@ -79,7 +77,7 @@ def main():
     rows = []
     for v in variants:
         t = np.array(res[v])
-        rows.append({"variant": dict(zip(("U", "CAP", "NTC", "REMAP", "IL"), v)), "median_ms": float(np.median(t)),
+        rows.append({"variant": dict(zip(FIELDS, v)), "median_ms": float(np.median(t)),
                      "min_ms": float(t.min()), "gbs_alg": bytes_alg / (np.median(t) * 1e-3) / 1e9,
                      "bit_identical": same[v]})
         print(json.dumps(rows[-1]), flush=True)
