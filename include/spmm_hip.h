@@ -14,10 +14,12 @@
  *        The engine computes on a ROW-major device copy (B[col][K]); host column-major input is transposed on
  *        the device, outside the SpMM kernel.
  *   C    y = C ROW-major: y[i*K + n] (spmm_kernel_csr.cpp:93); every entry is written (0 for empty rows).
- * Numerics: each C entry of a row with at most SPMM_HIP_SEQ_MAX nonzeros is one left-to-right fused
- * multiply-add chain from 0 over the row's nonzeros in CSR order -- the same bits as the reference kernel built
- * with its own flags on an FMA x86 host.  Longer rows are split into chunks whose partial sums are combined in a
- * fixed order (deterministic run to run; within 1e-10 relative normwise for fp64).
+ * Numerics: each C entry of a row with at most T nonzeros is one left-to-right fused multiply-add chain from 0
+ * over the row's nonzeros in CSR order -- the same bits as the reference kernel built with its own flags on an
+ * FMA x86 host.  T (the split length, reported by spmm_hip_info out[8]) is chosen by the inspector per matrix and K
+ * (16..2048) so every workgroup has enough independent rows; SPMM_HIP_SEQ_MAX=<n> fixes it.  Longer rows are cut
+ * into T-nonzero pieces whose partial sums are combined in piece order (deterministic run to run; within 1e-10
+ * relative normwise for fp64).
  */
 #ifndef SPMM_HIP_H
 #define SPMM_HIP_H
@@ -46,8 +48,8 @@ extern "C" {
 #define SPMM_HIP_B_COL_MAJOR  0   /* reference layout: x[n*ncols + col]                                    */
 #define SPMM_HIP_B_ROW_MAJOR  1   /* engine layout:   B[col*K + n]                                         */
 
-/* rows longer than this are split across workgroups (deterministic fixed-order combine) */
-#define SPMM_HIP_SEQ_MAX  4096
+/* upper bound of the split length T (the LDS capacity of one workgroup block, in nonzeros) */
+#define SPMM_HIP_SEQ_MAX  2048
 
 typedef struct spmm_hip_handle spmm_hip_t;
 
@@ -73,7 +75,8 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
  * (NULL = the null stream). */
 int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *d_c, int32_t k, void *stream);
 
-/* Plan for k without running (allocations happen here, not in run_device). */
+/* Plan for k without running: the inspector (lane layout, block capacity, split length T, K panels sized for the
+ * 256 MB Infinity Cache -- SPMM_HIP_PANEL_MB, default 192) and all allocations happen here, not in run_device. */
 int spmm_hip_plan(spmm_hip_t *h, int32_t k);
 
 /* Timing of the LAST run on the handle, from HIP events recorded on the run's stream (blocks until the run
@@ -84,12 +87,14 @@ int spmm_hip_last_times(spmm_hip_t *h, double *out_ms);
 /* Statistics: replaces statistics_print_labels / Matrix_Format::statistics_print_data
  * (spmv_kernel.h:20,30; spmv_bench.cpp:441-443,474-476).  Appends CSV columns to buf (at most buf_n bytes incl.
  * NUL) and returns the number of characters written (<0 on error).  Columns:
- *   kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,long_rows,device */
+ *   kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,split_rows,seq_max,panels,
+ *   device */
 int spmm_hip_stats_labels(char *buf, long buf_n);
 int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
 
-/* Static properties of the handle: out[0]=m, out[1]=ncols, out[2]=nnz, out[3]=k planned, out[4]=dtype,
- * out[5]=number of row blocks, out[6]=number of long-row chunks, out[7]=device bytes held. */
+/* Properties of the handle (out has 12 slots): out[0]=m, out[1]=ncols, out[2]=nnz, out[3]=k planned, out[4]=dtype,
+ * out[5]=workgroup blocks, out[6]=split rows, out[7]=device bytes held, out[8]=split length T (rows with <= T
+ * nonzeros are bit-exact), out[9]=block capacity, out[10]=K-panel width, out[11]=K panels. */
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
 
 /* Device buffers owned by the handle (for callers that stage B/C themselves), row-major B of the planned k. */

@@ -1,10 +1,22 @@
 // spmm_engine.hip -- C ABI (include/spmm_hip.h) of the MI355X-native CSR SpMM engine.
 //
 // Replaces the reference plugin surface (benchmark_code/CPU/AMD/spmv_code_bench/spmv_kernel.h:9-30):
-//   csr_to_format        -> spmm_hip_create   (inspector: validate, copy A to HBM, build the row-block table)
-//   Matrix_Format::spmm  -> spmm_hip_run      (host x/y, synchronous) / spmm_hip_run_device (HBM-resident)
+//   csr_to_format        -> spmm_hip_create + spmm_hip_plan   (validate, copy A to HBM, inspect)
+//   Matrix_Format::spmm  -> spmm_hip_run (host x/y, synchronous) / spmm_hip_run_device (HBM-resident)
 //   statistics_*         -> spmm_hip_stats_labels / spmm_hip_stats
 // Device kernels: spmm_kernels.hpp.
+//
+// The inspector (plan, per K; untimed like the reference's csr_to_format) decides the work shape from the matrix:
+//   * row group width G and lane width VEC from the K-panel width (16-byte lanes where the layout allows);
+//   * block capacity cap: 2048 nonzeros (the LDS capacity), smaller for small matrices so at least ~1024 blocks
+//     (4 per CU) exist;
+//   * split length T = clamp(cap / (256/G), 16, 2048): rows longer than T become ceil(len/T) virtual rows so a
+//     block always offers its 256/G row groups enough independent rows (long rows stop being serial chains of
+//     memory round trips).  Rows of <= T nonzeros are summed exactly like the reference (bit-identical); split
+//     rows are combined in slot order (deterministic).  SPMM_HIP_SEQ_MAX=<n> overrides T (n >= 2048 keeps every
+//     row <= 2048 bit-exact);
+//   * K panels: when B (ncols*K*s) exceeds the Infinity-Cache budget (SPMM_HIP_PANEL_MB, default 192), K is cut
+//     into power-of-two column panels whose B slice fits, one launch per panel (A is re-streamed per panel).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,15 +45,16 @@ int fail(int status, const std::string &what) {
     do {                                                                                                 \
         hipError_t _e = (expr);                                                                          \
         if (_e != hipSuccess)                                                                            \
-            return fail(SPMM_HIP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));            \
+            return fail(_e == hipErrorOutOfMemory ? SPMM_HIP_ERR_NOMEM : SPMM_HIP_ERR_HIP,                \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                              \
     } while (0)
 
-// Production kernel variant (chosen by tools/tune_kernel.py on MI355X; see DESIGN.md "Kernel tuning").
+constexpr int CAP = 2048;         // LDS capacity of a block (nonzeros)
+constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may read up to 3 elements past nnz)
+
+// Production kernel variant (tools/tune_kernel.py on MI355X).
 #ifndef DEF_U
 #define DEF_U 16
-#endif
-#ifndef DEF_CAP
-#define DEF_CAP 2048
 #endif
 #ifndef DEF_NTC
 #define DEF_NTC 1
@@ -49,17 +62,21 @@ int fail(int status, const std::string &what) {
 #ifndef DEF_REMAP
 #define DEF_REMAP 0
 #endif
-#ifndef DEF_IL
-#define DEF_IL 1
-#endif
 #ifndef DEF_BUF
 #define DEF_BUF 0
 #endif
 
 struct Plan {
     int k = -1;
-    int vec = 1;   // values per lane per load (16 B where K allows)
-    int g = 1;     // lanes per row group
+    int kw = 0, npanels = 0;   // panel width (columns) and count
+    int seq_max = 0;           // T
+    int cap = 0;               // block capacity (nonzeros)
+};
+
+struct Variant {
+    int u = DEF_U, ntc = DEF_NTC, remap = DEF_REMAP, buf = DEF_BUF;
+    int seq_max = 0, cap = 0;  // 0 = inspector policy
+    int64_t panel_bytes = 0;   // 0 = default / env
 };
 
 }  // namespace
@@ -69,153 +86,181 @@ struct spmm_hip_handle {
     int dtype = SPMM_HIP_F64;
     size_t vsize = 8;
     int64_t m = 0, ncols = 0, nnz = 0;
+    std::vector<int32_t> h_row_ptr;  // kept for re-inspection at plan time
 
-    // A in HBM
-    int32_t *d_row_ptr = nullptr;
     int32_t *d_col = nullptr;
     void *d_val = nullptr;
 
-    // inspector output (block capacity = the kernel variant's CAP)
-    int cap = 2048;
-    int variant[6] = {DEF_U, DEF_CAP, DEF_NTC, DEF_REMAP, DEF_IL, DEF_BUF};
-    std::vector<int32_t> h_row_ptr_copy;  // kept only by the tuning build (re-blocking for another CAP)
-    int nblk = 0;
-    int32_t *d_blk_rows = nullptr;
-    int nchunks = 0, nlong = 0;
-    int4 *d_chunks = nullptr;
+    // inspector output (per plan)
+    Plan plan;
+    Variant var;
+    int64_t nv = 0;                  // virtual rows
+    int nblk = 0, nlong = 0, nslots = 0;
+    int32_t *d_vrow_ptr = nullptr, *d_vdest = nullptr, *d_blk = nullptr;
     int4 *d_long_rows = nullptr;
-    std::vector<int4> h_chunks;
 
     // per-k buffers
-    Plan plan;
     void *d_b = nullptr;      // row-major B [ncols][k]
     void *d_xcol = nullptr;   // column-major staging for host uploads / device col-major input
     void *d_c = nullptr;      // row-major C [m][k]
-    void *d_part = nullptr;   // long-row partials [nchunks][k]
-    size_t b_bytes = 0, c_bytes = 0;
+    void *d_part = nullptr;   // split-row partials [nslots][k]
+    size_t b_bytes = 0, c_bytes = 0, insp_bytes = 0;
 
     const void *last_x = nullptr;
     hipStream_t stream = nullptr;  // own stream for spmm_hip_run
     hipEvent_t ev[8] = {};
     bool have_times = false, have_transpose = false, have_copies = false;
-    int64_t device_bytes = 0;
+    int64_t a_bytes = 0;
 };
 
 namespace {
 
-int next_pow2(int x) {
+int pow2_ceil(int64_t x) {
     int p = 1;
-    while (p < x) p <<= 1;
+    while (p < x && p < (1 << 30)) p <<= 1;
     return p;
 }
 
-Plan make_plan(int k, size_t vsize) {
-    Plan p;
-    p.k = k;
-    const size_t row_bytes = (size_t)k * vsize;
-    if (row_bytes % 16 == 0)
-        p.vec = (int)(16 / vsize);
-    else if (row_bytes % 8 == 0 && vsize <= 8)
-        p.vec = (int)(8 / vsize);
+int pow2_floor(int64_t x) {
+    int p = 1;
+    while ((int64_t)p * 2 <= x && p < (1 << 30)) p <<= 1;
+    return p;
+}
+
+int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+// Lane layout for a panel of `kw` columns with row stride `ld`: VEC values per lane (16-byte lanes when every lane
+// address stays 16-byte aligned), G lanes per row group (power of two, <= 64).
+void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
+    const size_t lb = (size_t)ld * vsize, wb = (size_t)kw * vsize;
+    if (lb % 16 == 0 && wb % 16 == 0)
+        vec = (int)(16 / vsize);
+    else if (lb % 8 == 0 && wb % 8 == 0 && vsize <= 8)
+        vec = (int)(8 / vsize);
     else
-        p.vec = 1;
-    if (p.vec < 1) p.vec = 1;
-    const int need = (k + p.vec - 1) / p.vec;
-    p.g = std::min(64, next_pow2(std::max(1, need)));
-    return p;
+        vec = 1;
+    g = std::min(64, pow2_ceil(std::max(1, (kw + vec - 1) / vec)));
 }
 
-template <typename T, int VEC, int G>
-void launch_long_path(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
-    if (h->nchunks > 0) {
-        spmm_long_chunks_kernel<T, VEC, G>
-            <<<h->nchunks, WG, 0, s>>>(h->d_col, (const T *)h->d_val, h->d_chunks, B, (T *)h->d_part, K);
-        const int64_t tot = (int64_t)h->nlong * K;
-        spmm_long_combine_kernel<T>
-            <<<(unsigned)((tot + WG - 1) / WG), WG, 0, s>>>(h->d_long_rows, h->nlong, (const T *)h->d_part, C, K);
-    }
+void free_plan(spmm_hip_t *h) {
+    void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
+    h->d_vrow_ptr = h->d_vdest = h->d_blk = nullptr;
+    h->d_long_rows = nullptr;
+    h->b_bytes = h->c_bytes = h->insp_bytes = 0;
+    h->plan = Plan();
+    h->nv = h->nblk = h->nlong = h->nslots = 0;
+    h->last_x = nullptr;
 }
 
-// 32-bit buffer offsets for the B gather are valid while B fits 4 GiB (else the flat 64-bit path is used).
-inline bool buf_ok(const spmm_hip_t *h) { return (uint64_t)h->ncols * (uint64_t)h->plan.k * h->vsize < (1ULL << 32); }
-
-template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, int IL, bool BUF>
-void launch_rows_v(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
-    if (h->nblk > 0) {
-        const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * K * sizeof(T), 0xFFFFFFFFull);
-        if (BUF && !buf_ok(h))
-            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, IL, false><<<h->nblk, WG, 0, s>>>(
-                h->d_row_ptr, h->d_col, (const T *)h->d_val, h->d_blk_rows, h->nblk, B, C, K, bb);
-        else
-            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, IL, BUF><<<h->nblk, WG, 0, s>>>(
-                h->d_row_ptr, h->d_col, (const T *)h->d_val, h->d_blk_rows, h->nblk, B, C, K, bb);
-    }
-    launch_long_path<T, VEC, G>(h, B, C, K, s);
+// ---------------------------------------------------------------------------------------------------- launches
+template <typename T, int VEC, int G, int U, bool NTC, bool REMAP, bool BUF>
+void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
+    const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * ld * sizeof(T), 0xFFFFFFFFull);
+    if (h->nslots > 0)
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, BUF, true><<<h->nblk, WG, 0, s>>>(
+            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
+    else
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, BUF, false><<<h->nblk, WG, 0, s>>>(
+            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
 }
+
+// 32-bit buffer offsets for the B gather are valid while B fits 4 GiB.
+inline bool buf_ok(const spmm_hip_t *h, int ld) { return (uint64_t)h->ncols * (uint64_t)ld * h->vsize < (1ULL << 32); }
 
 #ifdef SPMM_TUNING
-// Tuning build only: the K=32 fp64 shape (VEC=2, G=16) over a grid of variants, selected at run time.
-template <int U, int CAP, bool NTC, bool REMAP, int IL, bool BUF>
-bool try_variant(spmm_hip_t *h, const double *B, double *C, int K, hipStream_t s) {
-    const int *v = h->variant;
-    if (v[0] != U || v[1] != CAP || v[2] != (int)NTC || v[3] != (int)REMAP || v[4] != IL || v[5] != (int)BUF)
-        return false;
-    launch_rows_v<double, 2, 16, U, CAP, NTC, REMAP, IL, BUF>(h, B, C, K, s);
+// Tuning build only: a grid of row-kernel variants for the fp64 16-byte-lane shapes, selected at run time.
+template <typename T, int VEC, int G, int U, bool NTC, bool REMAP, bool BUF>
+bool try_variant(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
+    const Variant &v = h->var;
+    if (v.u != U || v.ntc != (int)NTC || v.remap != (int)REMAP || v.buf != (int)BUF) return false;
+    launch_rows_v<T, VEC, G, U, NTC, REMAP, BUF>(h, B, C, P, ld, kw, s);
     return true;
 }
-#define TV(U, CAP, NTC, REMAP, IL, BUF) try_variant<U, CAP, NTC, REMAP, IL, BUF>(h, B, C, K, s) ||
-bool launch_tuned(spmm_hip_t *h, const double *B, double *C, int K, hipStream_t s) {
-    return TV(8, 2048, true, false, 1, false) TV(16, 2048, true, false, 1, false) TV(16, 2048, true, false, 1, true)
-        TV(24, 2048, true, false, 1, true) TV(16, 1024, true, false, 1, true) TV(16, 2048, false, false, 1, true)
-        TV(16, 2048, true, true, 1, true) TV(8, 2048, true, false, 2, true) false;
+#define TV(U, NTC, REMAP, BUF) try_variant<T, VEC, G, U, NTC, REMAP, BUF>(h, B, C, P, ld, kw, s) ||
+template <typename T, int VEC, int G>
+bool launch_tuned(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
+    return TV(8, true, false, false) TV(16, true, false, false) TV(16, true, false, true) TV(24, true, false, false)
+        TV(16, false, false, false) TV(16, true, true, false) TV(8, true, false, true) false;
 }
 #endif
 
 template <typename T, int VEC, int G>
-void launch_rows_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
+void launch_rows_t(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
 #ifdef SPMM_TUNING
-    if constexpr (std::is_same<T, double>::value && VEC == 2 && G == 16) {
-        if (launch_tuned(h, B, C, K, s)) return;
+    if constexpr (std::is_same<T, double>::value && VEC == 2 && (G == 8 || G == 16)) {
+        if (launch_tuned<T, VEC, G>(h, B, C, P, ld, kw, s)) return;
     }
 #endif
-    launch_rows_v<T, VEC, G, DEF_U, DEF_CAP, (bool)DEF_NTC, (bool)DEF_REMAP, DEF_IL, (bool)DEF_BUF>(h, B, C, K, s);
+    if (DEF_BUF && !buf_ok(h, ld))
+        launch_rows_v<T, VEC, G, DEF_U, (bool)DEF_NTC, (bool)DEF_REMAP, false>(h, B, C, P, ld, kw, s);
+    else
+        launch_rows_v<T, VEC, G, DEF_U, (bool)DEF_NTC, (bool)DEF_REMAP, (bool)DEF_BUF>(h, B, C, P, ld, kw, s);
 }
 
 template <typename T, int VEC>
-void launch_rows_g(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
-    switch (h->plan.g) {
-        case 1: launch_rows_t<T, VEC, 1>(h, B, C, K, s); break;
-        case 2: launch_rows_t<T, VEC, 2>(h, B, C, K, s); break;
-        case 4: launch_rows_t<T, VEC, 4>(h, B, C, K, s); break;
-        case 8: launch_rows_t<T, VEC, 8>(h, B, C, K, s); break;
-        case 16: launch_rows_t<T, VEC, 16>(h, B, C, K, s); break;
-        case 32: launch_rows_t<T, VEC, 32>(h, B, C, K, s); break;
-        default: launch_rows_t<T, VEC, 64>(h, B, C, K, s); break;
+void launch_rows_g(spmm_hip_t *h, int g, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
+    switch (g) {
+        case 1: launch_rows_t<T, VEC, 1>(h, B, C, P, ld, kw, s); break;
+        case 2: launch_rows_t<T, VEC, 2>(h, B, C, P, ld, kw, s); break;
+        case 4: launch_rows_t<T, VEC, 4>(h, B, C, P, ld, kw, s); break;
+        case 8: launch_rows_t<T, VEC, 8>(h, B, C, P, ld, kw, s); break;
+        case 16: launch_rows_t<T, VEC, 16>(h, B, C, P, ld, kw, s); break;
+        case 32: launch_rows_t<T, VEC, 32>(h, B, C, P, ld, kw, s); break;
+        default: launch_rows_t<T, VEC, 64>(h, B, C, P, ld, kw, s); break;
+    }
+}
+
+template <typename T>
+void launch_panel(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
+    int vec, g;
+    lane_layout(kw, ld, sizeof(T), vec, g);
+    if (vec == 16 / (int)sizeof(T)) {
+        if constexpr (sizeof(T) == 8)
+            launch_rows_g<T, 2>(h, g, B, C, P, ld, kw, s);
+        else
+            launch_rows_g<T, 4>(h, g, B, C, P, ld, kw, s);
+    } else if (vec == 2 && sizeof(T) == 4) {
+        launch_rows_g<T, 2>(h, g, B, C, P, ld, kw, s);
+    } else {
+        launch_rows_g<T, 1>(h, g, B, C, P, ld, kw, s);
+    }
+}
+
+template <typename T>
+void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
+    T *P = (T *)h->d_part;
+    if (h->nblk > 0) {
+        for (int p = 0; p < h->plan.npanels; ++p) {
+            const int k0 = p * h->plan.kw;
+            const int kw = std::min(h->plan.kw, K - k0);
+            launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
+        }
+    }
+    if (h->nlong > 0) {
+        const int64_t tot = (int64_t)h->nlong * K;
+        spmm_combine_kernel<T><<<(unsigned)((tot + WG - 1) / WG), WG, 0, s>>>(h->d_long_rows, h->nlong, P, C, K);
     }
 }
 
 int launch_spmm(spmm_hip_t *h, const void *B, void *C, int K, hipStream_t s) {
-    if (h->dtype == SPMM_HIP_F64) {
-        if (h->plan.vec == 2)
-            launch_rows_g<double, 2>(h, (const double *)B, (double *)C, K, s);
-        else
-            launch_rows_g<double, 1>(h, (const double *)B, (double *)C, K, s);
-    } else {
-        if (h->plan.vec == 4)
-            launch_rows_g<float, 4>(h, (const float *)B, (float *)C, K, s);
-        else if (h->plan.vec == 2)
-            launch_rows_g<float, 2>(h, (const float *)B, (float *)C, K, s);
-        else
-            launch_rows_g<float, 1>(h, (const float *)B, (float *)C, K, s);
-    }
+    if (h->dtype == SPMM_HIP_F64)
+        launch_spmm_t<double>(h, (const double *)B, (double *)C, K, s);
+    else
+        launch_spmm_t<float>(h, (const float *)B, (float *)C, K, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SPMM_HIP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
     return SPMM_HIP_OK;
 }
 
 int launch_transpose(spmm_hip_t *h, const void *X, void *Bt, int K, hipStream_t s) {
-    dim3 grid((unsigned)((h->ncols + 63) / 64), (unsigned)((K + 31) / 32));
     if (h->ncols == 0 || K == 0) return SPMM_HIP_OK;
+    dim3 grid((unsigned)((h->ncols + 63) / 64), (unsigned)((K + 31) / 32));
     if (h->dtype == SPMM_HIP_F64)
         transpose_colmajor_kernel<double><<<grid, WG, 0, s>>>((const double *)X, (double *)Bt, h->ncols, K);
     else
@@ -225,57 +270,59 @@ int launch_transpose(spmm_hip_t *h, const void *X, void *Bt, int K, hipStream_t 
     return SPMM_HIP_OK;
 }
 
-void free_k_buffers(spmm_hip_t *h) {
-    if (h->d_b) (void)hipFree(h->d_b);
-    if (h->d_xcol) (void)hipFree(h->d_xcol);
-    if (h->d_c) (void)hipFree(h->d_c);
-    if (h->d_part) (void)hipFree(h->d_part);
-    h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
-    h->b_bytes = h->c_bytes = 0;
-    h->plan = Plan();
-    h->last_x = nullptr;
-}
+// ------------------------------------------------------------------------------------------------- inspector
+struct Inspection {
+    std::vector<int32_t> vrow_ptr, vdest, blk;
+    std::vector<int4> long_rows;
+    int nslots = 0;
+};
 
-// Inspector: greedy nnz-balanced row blocks (<= cap nonzeros, <= CAP_ROWS rows; a longer row is a block of
-// its own and is cut into CAP_LONG chunks for the long path).
-void build_blocks(const int32_t *rp, int64_t m, int cap, std::vector<int32_t> &blk, std::vector<int4> &chunks,
-                  std::vector<int4> &long_rows) {
-    blk.clear();
-    chunks.clear();
-    long_rows.clear();
-    blk.push_back(0);
-    int64_t r = 0;
-    while (r < m) {
+// Virtual rows (rows longer than T cut into T-nonzero pieces) packed greedily into blocks of <= cap nonzeros and
+// <= CAP_ROWS virtual rows.
+void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
+    out.vrow_ptr.clear();
+    out.vdest.clear();
+    out.blk.clear();
+    out.long_rows.clear();
+    out.nslots = 0;
+    out.vrow_ptr.reserve((size_t)m + 1);
+    out.vrow_ptr.push_back(rp[0]);
+    bool any_split = false;
+    for (int64_t r = 0; r < m; ++r) {
         const int64_t len = (int64_t)rp[r + 1] - rp[r];
-        if (len > cap) {
-            if (blk.back() != r) blk.push_back((int32_t)r);
-            const int nslot = (int)((len + CAP_LONG - 1) / CAP_LONG);
-            long_rows.push_back(make_int4((int)r, (int)chunks.size(), nslot, 0));
-            for (int q = 0; q < nslot; ++q) {
-                const int a = rp[r] + q * CAP_LONG;
-                const int e = (int)std::min<int64_t>((int64_t)a + CAP_LONG, rp[r + 1]);
-                chunks.push_back(make_int4((int)r, a, e, (int)chunks.size()));
+        if (len <= T) {
+            out.vrow_ptr.push_back(rp[r + 1]);
+            out.vdest.push_back((int32_t)r);
+        } else {
+            any_split = true;
+            const int pieces = (int)((len + T - 1) / T);
+            out.long_rows.push_back(make_int4((int)r, out.nslots, pieces, 0));
+            for (int q = 0; q < pieces; ++q) {
+                out.vrow_ptr.push_back((int32_t)std::min<int64_t>((int64_t)rp[r] + (int64_t)(q + 1) * T, rp[r + 1]));
+                out.vdest.push_back(-(out.nslots + q) - 1);
             }
-            blk.push_back((int32_t)(r + 1));
-            ++r;
-            continue;
+            out.nslots += pieces;
         }
-        int64_t start = blk.back();
-        int64_t nnz_blk = (int64_t)rp[r] - rp[start];
-        if (r - start >= CAP_ROWS || nnz_blk + len > cap) {
-            blk.push_back((int32_t)r);
-            continue;
-        }
-        ++r;
     }
-    if (blk.back() != m) blk.push_back((int32_t)m);
+    if (!any_split) out.vdest.clear();
+    const int64_t nv = (int64_t)out.vrow_ptr.size() - 1;
+    out.blk.push_back(0);
+    int64_t start = 0;
+    for (int64_t v = 0; v < nv; ++v) {
+        const int64_t len = (int64_t)out.vrow_ptr[v + 1] - out.vrow_ptr[v];
+        if (v > start && (v - start >= CAP_ROWS || (int64_t)out.vrow_ptr[v] - out.vrow_ptr[start] + len > cap)) {
+            out.blk.push_back((int32_t)v);
+            start = v;
+        }
+    }
+    if (nv > 0) out.blk.push_back((int32_t)nv);
 }
 
 }  // namespace
 
 extern "C" {
 
-const char *spmm_hip_version(void) { return "spmm-mi355x 0.1 (gfx950 row-block kernel)"; }
+const char *spmm_hip_version(void) { return "spmm-mi355x 0.2 (gfx950 virtual-row block kernel)"; }
 
 const char *spmm_hip_strerror(int s) {
     switch (s) {
@@ -296,8 +343,7 @@ const char *spmm_hip_last_error_detail(void) { return g_detail.c_str(); }
 int spmm_hip_device_count(int *count) {
     if (!count) return fail(SPMM_HIP_ERR_ARG, "count is NULL");
     int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess) n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     *count = n;
     return SPMM_HIP_OK;
 }
@@ -346,7 +392,7 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
     if (m < 0 || ncols < 0 || nnz < 0 || k < 0) return fail(SPMM_HIP_ERR_ARG, "negative size");
     if (dtype != SPMM_HIP_F64 && dtype != SPMM_HIP_F32) return fail(SPMM_HIP_ERR_ARG, "dtype");
     if (!row_ptr || (nnz > 0 && (!col_idx || !values))) return fail(SPMM_HIP_ERR_ARG, "null CSR array");
-    if (m >= INT32_MAX || ncols >= INT32_MAX || nnz >= INT32_MAX)
+    if (m >= INT32_MAX || ncols >= INT32_MAX || nnz >= INT32_MAX - 4096)
         return fail(SPMM_HIP_ERR_OVERFLOW, "m, ncols and nnz must fit int32 (reference INT_T = int32_t)");
     // validate the CSR (the reference trusts its input; we refuse malformed input instead of faulting the GPU)
     if (row_ptr[0] != 0 || row_ptr[m] != nnz) return fail(SPMM_HIP_ERR_CSR, "row_ptr[0] != 0 or row_ptr[m] != nnz");
@@ -368,17 +414,7 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
     h->m = m;
     h->ncols = ncols;
     h->nnz = nnz;
-
-    std::vector<int32_t> blk;
-    std::vector<int4> long_rows;
-    h->cap = DEF_CAP;
-    build_blocks(row_ptr, m, h->cap, blk, h->h_chunks, long_rows);
-#ifdef SPMM_TUNING
-    h->h_row_ptr_copy.assign(row_ptr, row_ptr + m + 1);
-#endif
-    h->nblk = (int)blk.size() - 1;
-    h->nchunks = (int)h->h_chunks.size();
-    h->nlong = (int)long_rows.size();
+    h->h_row_ptr.assign(row_ptr, row_ptr + m + 1);
 
     auto cleanup = [&](int st) {
         spmm_hip_destroy(h);
@@ -394,29 +430,16 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
         }                                                                                                \
     } while (0)
 
-    // col / val are padded by 64 B: the kernel stages 16-byte vectors from a 16-byte boundary (spmm_rows_kernel)
-    const size_t rp_b = (size_t)(m + 1) * 4, col_b = (size_t)std::max<int64_t>(nnz, 1) * 4 + 64,
-                 val_b = (size_t)std::max<int64_t>(nnz, 1) * h->vsize + 64, blk_b = blk.size() * 4;
-    HIPCHK_C(hipMalloc(&h->d_row_ptr, rp_b));
+    const size_t col_b = (size_t)nnz * 4 + PAD_BYTES, val_b = (size_t)nnz * h->vsize + PAD_BYTES;
     HIPCHK_C(hipMalloc(&h->d_col, col_b));
     HIPCHK_C(hipMalloc(&h->d_val, val_b));
-    HIPCHK_C(hipMalloc(&h->d_blk_rows, blk_b));
-    HIPCHK_C(hipMemcpy(h->d_row_ptr, row_ptr, rp_b, hipMemcpyHostToDevice));
     HIPCHK_C(hipMemset(h->d_col, 0, col_b));
     HIPCHK_C(hipMemset(h->d_val, 0, val_b));
     if (nnz > 0) {
         HIPCHK_C(hipMemcpy(h->d_col, col_idx, (size_t)nnz * 4, hipMemcpyHostToDevice));
         HIPCHK_C(hipMemcpy(h->d_val, values, (size_t)nnz * h->vsize, hipMemcpyHostToDevice));
     }
-    HIPCHK_C(hipMemcpy(h->d_blk_rows, blk.data(), blk_b, hipMemcpyHostToDevice));
-    h->device_bytes = (int64_t)(rp_b + col_b + val_b + blk_b);
-    if (h->nchunks > 0) {
-        HIPCHK_C(hipMalloc(&h->d_chunks, h->nchunks * sizeof(int4)));
-        HIPCHK_C(hipMalloc(&h->d_long_rows, h->nlong * sizeof(int4)));
-        HIPCHK_C(hipMemcpy(h->d_chunks, h->h_chunks.data(), h->nchunks * sizeof(int4), hipMemcpyHostToDevice));
-        HIPCHK_C(hipMemcpy(h->d_long_rows, long_rows.data(), h->nlong * sizeof(int4), hipMemcpyHostToDevice));
-        h->device_bytes += (int64_t)((h->nchunks + h->nlong) * sizeof(int4));
-    }
+    h->a_bytes = (int64_t)(col_b + val_b);
     HIPCHK_C(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     for (auto &e : h->ev) HIPCHK_C(hipEventCreate(&e));
 #undef HIPCHK_C
@@ -433,15 +456,59 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     if (h->plan.k == k) return SPMM_HIP_OK;
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    free_k_buffers(h);
-    h->plan = make_plan(k, h->vsize);
+    free_plan(h);
+
+    Plan pl;
+    pl.k = k;
+    // K panels sized for the Infinity Cache
+    const int64_t panel_bytes = h->var.panel_bytes > 0 ? h->var.panel_bytes
+                                                        : (int64_t)env_int("SPMM_HIP_PANEL_MB", 192) * (1 << 20);
+    const int min_kw = std::max(1, (int)(16 / h->vsize));
+    pl.kw = k;
+    if ((int64_t)h->ncols * k * (int64_t)h->vsize > panel_bytes && k > min_kw) {
+        const int64_t fit = panel_bytes / std::max<int64_t>(1, h->ncols * (int64_t)h->vsize);
+        pl.kw = std::max(min_kw, pow2_floor(std::max<int64_t>(fit, 1)));
+        if (pl.kw >= k) pl.kw = k;
+    }
+    pl.npanels = (k + pl.kw - 1) / pl.kw;
+    // block capacity and split length
+    int vec, g;
+    lane_layout(pl.kw, k, h->vsize, vec, g);
+    const int ng = WG / g;
+    pl.cap = h->var.cap > 0 ? h->var.cap : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
+    const int seq_env = env_int("SPMM_HIP_SEQ_MAX", 0);
+    pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max
+                 : seq_env > 0      ? seq_env
+                                    : std::max(16, pl.cap / ng);
+    pl.seq_max = std::min(pl.seq_max, pl.cap);
+
+    Inspection in;
+    inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in);
+    h->nv = (int64_t)in.vrow_ptr.size() - 1;
+    h->nblk = std::max(0, (int)in.blk.size() - 1);
+    h->nlong = (int)in.long_rows.size();
+    h->nslots = in.nslots;
+    h->plan = pl;
+
+    auto alloc_copy = [&](void **dst, const void *src, size_t bytes) -> hipError_t {
+        hipError_t e = hipMalloc(dst, std::max<size_t>(bytes, 4));
+        if (e == hipSuccess && bytes > 0) e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+        return e;
+    };
+    hipError_t e = alloc_copy((void **)&h->d_vrow_ptr, in.vrow_ptr.data(), in.vrow_ptr.size() * 4);
+    if (e == hipSuccess) e = alloc_copy((void **)&h->d_blk, in.blk.data(), in.blk.size() * 4);
+    if (e == hipSuccess && !in.vdest.empty()) e = alloc_copy((void **)&h->d_vdest, in.vdest.data(), in.vdest.size() * 4);
+    if (e == hipSuccess && h->nlong > 0)
+        e = alloc_copy((void **)&h->d_long_rows, in.long_rows.data(), in.long_rows.size() * sizeof(int4));
+    h->insp_bytes = (in.vrow_ptr.size() + in.blk.size() + in.vdest.size()) * 4 + in.long_rows.size() * sizeof(int4);
     h->b_bytes = (size_t)std::max<int64_t>(h->ncols, 1) * k * h->vsize;
     h->c_bytes = (size_t)std::max<int64_t>(h->m, 1) * k * h->vsize;
-    hipError_t e;
-    if ((e = hipMalloc(&h->d_b, h->b_bytes)) != hipSuccess ||
-        (e = hipMalloc(&h->d_xcol, h->b_bytes)) != hipSuccess || (e = hipMalloc(&h->d_c, h->c_bytes)) != hipSuccess ||
-        (h->nchunks > 0 && (e = hipMalloc(&h->d_part, (size_t)h->nchunks * k * h->vsize)) != hipSuccess)) {
-        free_k_buffers(h);
+    if (e == hipSuccess) e = hipMalloc(&h->d_b, h->b_bytes);
+    if (e == hipSuccess) e = hipMalloc(&h->d_xcol, h->b_bytes);
+    if (e == hipSuccess) e = hipMalloc(&h->d_c, h->c_bytes);
+    if (e == hipSuccess && h->nslots > 0) e = hipMalloc(&h->d_part, (size_t)h->nslots * k * h->vsize);
+    if (e != hipSuccess) {
+        free_plan(h);
         return fail(e == hipErrorOutOfMemory ? SPMM_HIP_ERR_NOMEM : SPMM_HIP_ERR_HIP,
                     std::string("plan alloc: ") + hipGetErrorString(e));
     }
@@ -492,9 +559,8 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k) {
     const char *env = getenv("SPMM_HIP_ASSUME_X_UNCHANGED");
     const bool reuse = env && env[0] == '1' && x == h->last_x;
     HIPCHK(hipEventRecord(h->ev[4], s));
-    if (!reuse && h->ncols > 0) {
+    if (!reuse && h->ncols > 0)
         HIPCHK(hipMemcpyAsync(h->d_xcol, x, (size_t)h->ncols * k * h->vsize, hipMemcpyHostToDevice, s));
-    }
     HIPCHK(hipEventRecord(h->ev[5], s));
     HIPCHK(hipEventRecord(h->ev[2], s));
     if (!reuse) {
@@ -541,8 +607,9 @@ int spmm_hip_last_times(spmm_hip_t *h, double *out_ms) {
 int spmm_hip_stats_labels(char *buf, long buf_n) {
     if (!buf || buf_n <= 0) return fail(SPMM_HIP_ERR_ARG, "stats_labels: buffer");
     int n = snprintf(buf, (size_t)buf_n,
-                     ",kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,long_rows,device");
-    return std::min<long>(n, buf_n - 1);
+                     ",kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,split_rows,"
+                     "seq_max,panels,device");
+    return (int)std::min<long>(n, buf_n - 1);
 }
 
 int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n) {
@@ -553,9 +620,9 @@ int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n) {
     const int k = h->plan.k > 0 ? h->plan.k : 0;
     const double bytes = spmm_hip_bytes_alg(h->m, h->ncols, h->nnz, k, h->dtype);
     const double gbs = t[0] > 0 ? bytes / (t[0] * 1e-3) / 1e9 : 0.0;
-    int n = snprintf(buf, (size_t)buf_n, ",%.6f,%.6f,%.6f,%.6f,%.0f,%.2f,%.4f,%d,%d,%d", t[0], t[1], t[2], t[3], bytes,
-                     gbs, gbs / 8000.0, h->nblk, h->nlong, h->device);
-    return std::min<long>(n, buf_n - 1);
+    int n = snprintf(buf, (size_t)buf_n, ",%.6f,%.6f,%.6f,%.6f,%.0f,%.2f,%.4f,%d,%d,%d,%d,%d", t[0], t[1], t[2], t[3],
+                     bytes, gbs, gbs / 8000.0, h->nblk, h->nlong, h->plan.seq_max, h->plan.npanels, h->device);
+    return (int)std::min<long>(n, buf_n - 1);
 }
 
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
@@ -566,8 +633,13 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
     out[3] = h->plan.k;
     out[4] = h->dtype;
     out[5] = h->nblk;
-    out[6] = h->nchunks;
-    out[7] = h->device_bytes + (int64_t)(2 * h->b_bytes + h->c_bytes);
+    out[6] = h->nlong;
+    out[7] = h->a_bytes + (int64_t)(h->insp_bytes + 2 * h->b_bytes + h->c_bytes) +
+             (int64_t)h->nslots * std::max(h->plan.k, 0) * (int64_t)h->vsize;
+    out[8] = h->plan.seq_max;
+    out[9] = h->plan.cap;
+    out[10] = h->plan.kw;
+    out[11] = h->plan.npanels;
     return SPMM_HIP_OK;
 }
 
@@ -582,13 +654,9 @@ int spmm_hip_destroy(spmm_hip_t *h) {
     if (!h) return SPMM_HIP_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    free_k_buffers(h);
-    if (h->d_row_ptr) (void)hipFree(h->d_row_ptr);
+    free_plan(h);
     if (h->d_col) (void)hipFree(h->d_col);
     if (h->d_val) (void)hipFree(h->d_val);
-    if (h->d_blk_rows) (void)hipFree(h->d_blk_rows);
-    if (h->d_chunks) (void)hipFree(h->d_chunks);
-    if (h->d_long_rows) (void)hipFree(h->d_long_rows);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -597,44 +665,20 @@ int spmm_hip_destroy(spmm_hip_t *h) {
 }
 
 #ifdef SPMM_TUNING
-// Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): pick the K=32 fp64 row-kernel variant and
-// rebuild the row-block table for its capacity.
-int spmm_hip_tune_select(spmm_hip_t *h, int u, int cap, int ntc, int remap, int il, int buf) {
-    if (!h || h->h_row_ptr_copy.empty()) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
-    HIPCHK(hipSetDevice(h->device));
-    HIPCHK(hipDeviceSynchronize());
-    std::vector<int32_t> blk;
-    std::vector<int4> long_rows;
-    build_blocks(h->h_row_ptr_copy.data(), h->m, cap, blk, h->h_chunks, long_rows);
-    if (h->d_blk_rows) (void)hipFree(h->d_blk_rows);
-    if (h->d_chunks) (void)hipFree(h->d_chunks);
-    if (h->d_long_rows) (void)hipFree(h->d_long_rows);
-    h->d_blk_rows = nullptr;
-    h->d_chunks = nullptr;
-    h->d_long_rows = nullptr;
-    h->nblk = (int)blk.size() - 1;
-    h->nchunks = (int)h->h_chunks.size();
-    h->nlong = (int)long_rows.size();
-    HIPCHK(hipMalloc(&h->d_blk_rows, blk.size() * 4));
-    HIPCHK(hipMemcpy(h->d_blk_rows, blk.data(), blk.size() * 4, hipMemcpyHostToDevice));
-    if (h->nchunks > 0) {
-        HIPCHK(hipMalloc(&h->d_chunks, h->nchunks * sizeof(int4)));
-        HIPCHK(hipMalloc(&h->d_long_rows, h->nlong * sizeof(int4)));
-        HIPCHK(hipMemcpy(h->d_chunks, h->h_chunks.data(), h->nchunks * sizeof(int4), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(h->d_long_rows, long_rows.data(), h->nlong * sizeof(int4), hipMemcpyHostToDevice));
-        if (h->plan.k > 0) {
-            if (h->d_part) (void)hipFree(h->d_part);
-            HIPCHK(hipMalloc(&h->d_part, (size_t)h->nchunks * h->plan.k * h->vsize));
-        }
-    }
-    h->cap = cap;
-    h->variant[0] = u;
-    h->variant[1] = cap;
-    h->variant[2] = ntc;
-    h->variant[3] = remap;
-    h->variant[4] = il;
-    h->variant[5] = buf;
-    return SPMM_HIP_OK;
+// Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): kernel variant + inspector overrides; the
+// next run re-plans.  0 = policy default for seq_max / cap / panel_mb.
+int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int remap, int buf, int seq_max, int cap, int panel_mb) {
+    if (!h) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
+    h->var.u = u;
+    h->var.ntc = ntc;
+    h->var.remap = remap;
+    h->var.buf = buf;
+    h->var.seq_max = seq_max;
+    h->var.cap = cap;
+    h->var.panel_bytes = (int64_t)panel_mb * (1 << 20);
+    const int k = h->plan.k;
+    h->plan.k = -1;
+    return k > 0 ? spmm_hip_plan(h, k) : SPMM_HIP_OK;
 }
 #endif
 

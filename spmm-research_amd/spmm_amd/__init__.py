@@ -23,7 +23,7 @@ LIB_DIR = PKG_ROOT / "lib"
 
 F64, F32 = 0, 1
 B_COL_MAJOR, B_ROW_MAJOR = 0, 1
-SEQ_MAX = 2048
+SEQ_MAX = 2048      # upper bound of the per-handle split length (MatrixFormat.seq_max)
 STATUS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP runtime error", -4: "no such HIP device",
           -5: "k mismatch", -6: "malformed CSR", -7: "size overflow"}
 
@@ -332,9 +332,14 @@ class MatrixFormat:
         return {"kernel_ms": t[0], "transpose_ms": t[1], "h2d_ms": t[2], "d2h_ms": t[3]}
 
     def info(self) -> np.ndarray:
-        out = np.zeros(8, np.int64)
+        out = np.zeros(12, np.int64)
         _check("info", hip.spmm_hip_info(self._h, out))
         return out
+
+    @property
+    def seq_max(self) -> int:
+        """Split length T of the current plan: rows with <= T nonzeros are bit-identical to the reference."""
+        return int(self.info()[8])
 
     def statistics_start(self) -> None:
         pass

@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""tools/sweep.py -- dataset sweep driver (BASELINE configs 3/4: synthetic medium / large datasets, K sweep).
+
+For each generator line (from tools/medium_dataset.py, a file, or --line): generate the matrix once on the host,
+build one engine handle, and for every K: B = seeded U[0,1) resident in HBM (row-major), time `--iters` launches
+with HIP events on the launch stream (after `--warmup`), and check a sample of rows against the CPU oracle
+(bit-exact for rows <= the handle's split length T, normwise 1e-10 beyond).  One JSON line per (matrix, K) appended to --out; lines
+already present are skipped, so an interrupted sweep resumes where it stopped.  --budget bounds the wall time.
+
+  python tools/sweep.py --dataset medium --stride 60 --k 1,8,32,128 --out gpurun_out/sweep_medium.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "spmm-research_amd"))
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tools"))
+
+
+def dataset_lines(args) -> list[str]:
+    if args.line:
+        return list(args.line)
+    if args.dataset == "medium":
+        from medium_dataset import medium_dataset_lines
+        lines = medium_dataset_lines()
+    else:
+        lines = [l.strip() for l in open(args.dataset) if l.strip()]
+    if args.sort_by_size:
+        lines.sort(key=lambda l: int(l.split()[0]) * float(l.split()[2]))
+    return lines[args.offset::args.stride]
+
+
+def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, seq_max):
+    """Oracle on a row sample: sub-CSR of the sampled rows with its columns renumbered, B rows fetched from HBM."""
+    import torch
+    m = A.m
+    deg = np.diff(A.row_ptr)
+    rows = np.unique(np.concatenate([rng.choice(m, min(nsample, m), replace=False), [int(np.argmax(deg))]]))
+    sub_rp = np.zeros(len(rows) + 1, np.int32)
+    sub_rp[1:] = np.cumsum(deg[rows])
+    cols = np.concatenate([A.col_idx[A.row_ptr[r]:A.row_ptr[r + 1]] for r in rows]) if sub_rp[-1] else np.zeros(0, np.int32)
+    vals = np.concatenate([A.values[A.row_ptr[r]:A.row_ptr[r + 1]] for r in rows]) if sub_rp[-1] else np.zeros(0)
+    ucols, inv = np.unique(cols, return_inverse=True)
+    bsub = B_dev.index_select(0, torch.from_numpy(ucols.astype(np.int64)).to(B_dev.device)).cpu().numpy()
+    x_col = np.ascontiguousarray(bsub.T).ravel()                 # column-major [k][ncols_sub]
+    vv = vals.astype(dtype)
+    want = O.spmm(sub_rp, inv.astype(np.int32), vv, len(ucols), x_col.astype(dtype), k)
+    got = C_dev.index_select(0, torch.from_numpy(rows.astype(np.int64)).to(C_dev.device)).cpu().numpy()
+    seq = deg[rows] <= seq_max
+    it = np.int64 if dtype == np.float64 else np.int32
+    bit_ok = bool(np.array_equal(got[seq].view(it), want[seq].view(it)))
+    g, absdot = O.gold(sub_rp, inv.astype(np.int32), vals, len(ucols), x_col.astype(np.float64), k)
+    if dtype == np.float64:
+        norm_ok = bool(O.normwise_ok(got, g, absdot, 1e-10).all())
+    else:   # fp32 sequential sums: gamma_n ~ n * 2^-24 per row
+        tol = 2.0 * np.maximum(deg[rows], 1)[:, None] * 2.0 ** -24
+        norm_ok = bool((np.abs(got.astype(np.float64) - g) <= tol * np.maximum(np.abs(g), absdot)).all())
+    return {"rows_checked": int(len(rows)), "bitexact_seq_rows": bit_ok, "normwise_ok": norm_ok,
+            "long_rows_checked": int((~seq).sum())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dataset", default="medium", help="'medium' or a path to a file of generator lines")
+    ap.add_argument("--line", action="append", help="explicit generator line(s) instead of a dataset")
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--offset", type=int, default=0)
+    ap.add_argument("--sort-by-size", action="store_true")
+    ap.add_argument("--k", default="32")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--check-rows", type=int, default=256)
+    ap.add_argument("--max-nnz", type=float, default=2.0e8)
+    ap.add_argument("--budget", type=float, default=1e9, help="seconds; stop starting new matrices after this")
+    ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "sweep.jsonl"))
+    args = ap.parse_args()
+
+    import torch
+    import spmm_amd as S
+    from oracle import oracle as O
+
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    dtype = np.float64 if args.dtype == "f64" else np.float32
+    tdtype = torch.float64 if args.dtype == "f64" else torch.float32
+    ks = [int(x) for x in args.k.split(",")]
+    out = Path(args.out)
+    out.parent.mkdir(parents=True, exist_ok=True)
+    done = set()
+    if out.exists():
+        for l in out.read_text().splitlines():
+            try:
+                d = json.loads(l)
+                done.add((d["gen"], d["k"], d["dtype"]))
+            except Exception:
+                pass
+    t_start = time.time()
+    rng = np.random.default_rng(0)
+    for li, line in enumerate(dataset_lines(args)):
+        todo = [k for k in ks if (line, k, args.dtype) not in done]
+        if not todo:
+            continue
+        if time.time() - t_start > args.budget:
+            print(f"budget reached after {li} lines", flush=True)
+            break
+        p = S.gen_params(line)
+        if p.nr_rows * p.avg_nnz_per_row > args.max_nnz:
+            continue
+        t0 = time.time()
+        A = S.generate(p)
+        t_gen = time.time() - t0
+        feat = S.features(A)
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(dtype), A.m, A.ncols, A.nnz, 0, 0)
+        for k in todo:
+            mf.plan(k)
+            g = torch.Generator(device=dev)
+            g.manual_seed(42)
+            B = torch.rand((A.ncols, k), generator=g, device=dev, dtype=tdtype)
+            Cm = torch.empty((A.m, k), device=dev, dtype=tdtype)
+            run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
+            for _ in range(args.warmup):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(args.iters):
+                run()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.iters
+            bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
+            par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.seq_max)
+            inf = mf.info()
+            rec = {"gen": line, "k": k, "dtype": args.dtype, "m": int(A.m), "nnz": int(A.nnz), "ms": ms,
+                   "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9, "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9,
+                   "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12, "mem_mb": feat["mem_footprint"],
+                   "features": {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled", "skew",
+                                                     "avg_num_neighbours", "cross_row_similarity")},
+                   "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]),
+                   "split_rows": int(inf[6]), "blocks": int(inf[5]), **par}
+            with open(out, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+            print(json.dumps({k2: rec[k2] for k2 in ("gen", "k", "ms", "gflops", "roofline_frac",
+                                                     "bitexact_seq_rows", "normwise_ok")}), flush=True)
+            del B, Cm
+        mf.close()
+        del A
+
+
+if __name__ == "__main__":
+    main()
