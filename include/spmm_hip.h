@@ -17,7 +17,7 @@
  * Numerics: each C entry of a row with at most T nonzeros is one left-to-right fused multiply-add chain from 0
  * over the row's nonzeros in CSR order -- the same bits as the reference kernel built with its own flags on an
  * FMA x86 host.  T (the split length, reported by spmm_hip_info out[8]) is chosen by the inspector per matrix and K
- * (16..2048) so every workgroup has enough independent rows; SPMM_HIP_SEQ_MAX=<n> fixes it.  Longer rows are cut
+ * (64..2048) so no serial row outlasts the launch; SPMM_HIP_SEQ_MAX=<n> fixes it.  Longer rows are cut
  * into T-nonzero pieces whose partial sums are combined in piece order (deterministic run to run; within 1e-10
  * relative normwise for fp64).
  */
@@ -75,8 +75,9 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
  * (NULL = the null stream). */
 int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *d_c, int32_t k, void *stream);
 
-/* Plan for k without running: the inspector (lane layout, block capacity, split length T, K panels sized for the
- * 256 MB Infinity Cache -- SPMM_HIP_PANEL_MB, default 192) and all allocations happen here, not in run_device. */
+/* Plan for k without running: the inspector (lane layout, block capacity, split length T, K panels of 256-byte B
+ * rows when B would crowd the Infinity Cache -- SPMM_HIP_PANEL_K=<cols> overrides) and all allocations happen here, not in
+ * run_device. */
 int spmm_hip_plan(spmm_hip_t *h, int32_t k);
 
 /* Timing of the LAST run on the handle, from HIP events recorded on the run's stream (blocks until the run
@@ -92,7 +93,9 @@ int spmm_hip_last_times(spmm_hip_t *h, double *out_ms);
 int spmm_hip_stats_labels(char *buf, long buf_n);
 int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
 
-/* Properties of the handle (out has 12 slots): out[0]=m, out[1]=ncols, out[2]=nnz, out[3]=k planned, out[4]=dtype,
+#define SPMM_HIP_INFO_SLOTS 12
+
+/* Properties of the handle (out has SPMM_HIP_INFO_SLOTS = 12 slots): out[0]=m, out[1]=ncols, out[2]=nnz, out[3]=k planned, out[4]=dtype,
  * out[5]=workgroup blocks, out[6]=split rows, out[7]=device bytes held, out[8]=split length T (rows with <= T
  * nonzeros are bit-exact), out[9]=block capacity, out[10]=K-panel width, out[11]=K panels. */
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out);

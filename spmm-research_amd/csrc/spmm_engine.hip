@@ -10,13 +10,14 @@
 //   * row group width G and lane width VEC from the K-panel width (16-byte lanes where the layout allows);
 //   * block capacity cap: 2048 nonzeros (the LDS capacity), smaller for small matrices so at least ~1024 blocks
 //     (4 per CU) exist;
-//   * split length T = clamp(cap / (256/G), 16, 2048): rows longer than T become ceil(len/T) virtual rows so a
-//     block always offers its 256/G row groups enough independent rows (long rows stop being serial chains of
-//     memory round trips).  Rows of <= T nonzeros are summed exactly like the reference (bit-identical); split
-//     rows are combined in slot order (deterministic).  SPMM_HIP_SEQ_MAX=<n> overrides T (n >= 2048 keeps every
-//     row <= 2048 bit-exact);
-//   * K panels: when B (ncols*K*s) exceeds the Infinity-Cache budget (SPMM_HIP_PANEL_MB, default 192), K is cut
-//     into power-of-two column panels whose B slice fits, one launch per panel (A is re-streamed per panel).
+//   * split length T (split_length(): 64..2048 from a time model of the launch): rows longer than T become
+//     ceil(len/T) virtual rows so no serial chain of memory round trips outlasts the rest of the grid; blocks
+//     holding long rows are dispatched first.  Rows of <= T nonzeros are summed exactly like the reference
+//     (bit-identical); split rows are combined in slot order (deterministic).  SPMM_HIP_SEQ_MAX=<n> overrides T
+//     (n >= 2048 keeps every row <= 2048 bit-exact);
+//   * K panels: when B (ncols*K*s) would crowd the Infinity Cache (> 128 MB) and the gather dominates (>= 16
+//     nonzeros per row), K is cut into panels of 256-byte B rows (32 fp64 / 64 fp32 columns; SPMM_HIP_PANEL_K=<cols>
+//     overrides), one launch per panel (A is re-streamed per panel).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -59,11 +60,11 @@ constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may
 #ifndef DEF_NTC
 #define DEF_NTC 1
 #endif
-#ifndef DEF_REMAP
-#define DEF_REMAP 0
+#ifndef DEF_DMA
+#define DEF_DMA 0
 #endif
 #ifndef DEF_BUF
-#define DEF_BUF 0
+#define DEF_BUF 1
 #endif
 
 struct Plan {
@@ -74,9 +75,9 @@ struct Plan {
 };
 
 struct Variant {
-    int u = DEF_U, ntc = DEF_NTC, remap = DEF_REMAP, buf = DEF_BUF;
+    int u = DEF_U, ntc = DEF_NTC, dma = DEF_DMA, buf = DEF_BUF;
     int seq_max = 0, cap = 0;  // 0 = inspector policy
-    int64_t panel_bytes = 0;   // 0 = default / env
+    int panel_k = 0;           // 0 = inspector policy
 };
 
 }  // namespace
@@ -96,7 +97,8 @@ struct spmm_hip_handle {
     Variant var;
     int64_t nv = 0;                  // virtual rows
     int nblk = 0, nlong = 0, nslots = 0;
-    int32_t *d_vrow_ptr = nullptr, *d_vdest = nullptr, *d_blk = nullptr;
+    int32_t *d_vrow_ptr = nullptr, *d_vdest = nullptr;
+    int2 *d_blk = nullptr;
     int4 *d_long_rows = nullptr;
 
     // per-k buffers
@@ -121,11 +123,6 @@ int pow2_ceil(int64_t x) {
     return p;
 }
 
-int pow2_floor(int64_t x) {
-    int p = 1;
-    while ((int64_t)p * 2 <= x && p < (1 << 30)) p <<= 1;
-    return p;
-}
 
 int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
@@ -150,7 +147,8 @@ void free_plan(spmm_hip_t *h) {
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
-    h->d_vrow_ptr = h->d_vdest = h->d_blk = nullptr;
+    h->d_vrow_ptr = h->d_vdest = nullptr;
+    h->d_blk = nullptr;
     h->d_long_rows = nullptr;
     h->b_bytes = h->c_bytes = h->insp_bytes = 0;
     h->plan = Plan();
@@ -159,15 +157,17 @@ void free_plan(spmm_hip_t *h) {
 }
 
 // ---------------------------------------------------------------------------------------------------- launches
-template <typename T, int VEC, int G, int U, bool NTC, bool REMAP, bool BUF>
+template <typename T, int VEC, int G, int U, bool NTC, bool DMA, bool BUF>
 void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
     const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * ld * sizeof(T), 0xFFFFFFFFull);
+    auto go = [&](auto split_c) {
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(split_c)::value><<<h->nblk, WG, 0, s>>>(
+            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
+    };
     if (h->nslots > 0)
-        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, BUF, true><<<h->nblk, WG, 0, s>>>(
-            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
+        go(std::true_type());
     else
-        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, REMAP, BUF, false><<<h->nblk, WG, 0, s>>>(
-            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
+        go(std::false_type());
 }
 
 // 32-bit buffer offsets for the B gather are valid while B fits 4 GiB.
@@ -175,32 +175,37 @@ inline bool buf_ok(const spmm_hip_t *h, int ld) { return (uint64_t)h->ncols * (u
 
 #ifdef SPMM_TUNING
 // Tuning build only: a grid of row-kernel variants for the fp64 16-byte-lane shapes, selected at run time.
-template <typename T, int VEC, int G, int U, bool NTC, bool REMAP, bool BUF>
+template <typename T, int VEC, int G, int U, bool NTC, bool DMA, bool BUF>
 bool try_variant(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
     const Variant &v = h->var;
-    if (v.u != U || v.ntc != (int)NTC || v.remap != (int)REMAP || v.buf != (int)BUF) return false;
-    launch_rows_v<T, VEC, G, U, NTC, REMAP, BUF>(h, B, C, P, ld, kw, s);
+    if (v.u != U || v.ntc != (int)NTC || v.dma != (int)DMA || v.buf != (int)BUF) return false;
+    launch_rows_v<T, VEC, G, U, NTC, DMA, BUF>(h, B, C, P, ld, kw, s);
     return true;
 }
-#define TV(U, NTC, REMAP, BUF) try_variant<T, VEC, G, U, NTC, REMAP, BUF>(h, B, C, P, ld, kw, s) ||
+#define TV(U, NTC, DMA, BUF) try_variant<T, VEC, G, U, NTC, DMA, BUF>(h, B, C, P, ld, kw, s) ||
 template <typename T, int VEC, int G>
 bool launch_tuned(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
-    return TV(8, true, false, false) TV(16, true, false, false) TV(16, true, false, true) TV(24, true, false, false)
-        TV(16, false, false, false) TV(16, true, true, false) TV(8, true, false, true) false;
+    return TV(16, true, true, false) TV(16, true, false, false) TV(8, true, true, false) TV(8, true, false, false)
+        TV(24, true, true, false) TV(16, true, true, true) TV(16, true, false, true) TV(16, false, true, false) false;
 }
 #endif
 
 template <typename T, int VEC, int G>
 void launch_rows_t(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
 #ifdef SPMM_TUNING
-    if constexpr (std::is_same<T, double>::value && VEC == 2 && (G == 8 || G == 16)) {
+    if constexpr (std::is_same<T, double>::value && ((VEC == 2 && G >= 4 && G <= 32) || (VEC == 1 && G == 1))) {
         if (launch_tuned<T, VEC, G>(h, B, C, P, ld, kw, s)) return;
     }
 #endif
-    if (DEF_BUF && !buf_ok(h, ld))
-        launch_rows_v<T, VEC, G, DEF_U, (bool)DEF_NTC, (bool)DEF_REMAP, false>(h, B, C, P, ld, kw, s);
+    // One-lane row groups (K = 1): LDS-DMA staging and flat gathers (0.086 vs 0.121 ms on config 2, K=1); wider
+    // groups: staging through VGPRs and 32-bit buffer-offset gathers (config 2 K=32 0.404 vs 0.420 ms; 500-nnz rows
+    // K=8 2.10 vs 2.91 ms) -- DESIGN.md §6.2.
+    constexpr bool dma = G == 1 ? true : (bool)DEF_DMA;
+    constexpr bool buf = G == 1 ? false : (bool)DEF_BUF;
+    if (buf && !buf_ok(h, ld))
+        launch_rows_v<T, VEC, G, DEF_U, (bool)DEF_NTC, dma, false>(h, B, C, P, ld, kw, s);
     else
-        launch_rows_v<T, VEC, G, DEF_U, (bool)DEF_NTC, (bool)DEF_REMAP, (bool)DEF_BUF>(h, B, C, P, ld, kw, s);
+        launch_rows_v<T, VEC, G, DEF_U, (bool)DEF_NTC, dma, buf>(h, B, C, P, ld, kw, s);
 }
 
 template <typename T, int VEC>
@@ -243,8 +248,12 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         }
     }
     if (h->nlong > 0) {
+#ifdef SPMM_EXP_SERIAL_COMBINE
         const int64_t tot = (int64_t)h->nlong * K;
-        spmm_combine_kernel<T><<<(unsigned)((tot + WG - 1) / WG), WG, 0, s>>>(h->d_long_rows, h->nlong, P, C, K);
+        spmm_combine_serial_kernel<T><<<(unsigned)((tot + WG - 1) / WG), WG, 0, s>>>(h->d_long_rows, h->nlong, P, C, K);
+#else
+        spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
+#endif
     }
 }
 
@@ -271,9 +280,32 @@ int launch_transpose(spmm_hip_t *h, const void *X, void *Bt, int K, hipStream_t 
 }
 
 // ------------------------------------------------------------------------------------------------- inspector
+// Split length T.  A row is one serial chain of len/U dependent gather batches; measured on MI355X (§6.2) a chain
+// advances ~5.5 nonzeros/us under load, and a launch takes about est' = 1.3 * (gathered B rows at ~12 TB/s incl.
+// L2 hits + A and C streamed at ~6 TB/s) + 10 us.  Rows whose chain would outlast the launch are split (their
+// blocks are dispatched first, see inspect()); rows within 2.5x of the mean are never split (splitting them
+// balances nothing and adds partial-sum traffic), unless the matrix has too few rows to give every CU work
+// (m < 2048), where every row is cut so the row groups of a block have work.  T is clamped to [64, 2048].
+// Rows <= T stay a single FMA chain, bit-identical to the reference; config 2 (T = 2048) is exact throughout.
+constexpr double CHAIN_NNZ_PER_US = 5.5;
+int split_length(const spmm_hip_t *h, int kw) {
+    const double s = (double)h->vsize;
+    const double est_us = 1.3 * ((double)h->nnz * kw * s / 12.0e6 +
+                                 ((double)h->nnz * (4.0 + s) + (double)h->m * kw * s + 4.0 * h->m) / 6.0e6) + 10.0;
+    double t = CHAIN_NNZ_PER_US * est_us * (double)h->var.u / 16.0;
+    if (h->m >= 2048) t = std::max(t, 2.5 * (double)h->nnz / (double)std::max<int64_t>(h->m, 1));
+    return (int)std::max(64.0, std::min((double)CAP, t));
+}
+
+constexpr int64_t PANEL_ROW_BYTES = 256;          // B bytes per row of one K panel
+constexpr double PANEL_MIN_B_BYTES = 128.0 * (1 << 20);  // B below half the Infinity Cache: no panels
+constexpr double PANEL_MIN_ROW_NNZ = 16.0;
+
 struct Inspection {
-    std::vector<int32_t> vrow_ptr, vdest, blk;
+    std::vector<int32_t> vrow_ptr, vdest;
+    std::vector<int2> blk;
     std::vector<int4> long_rows;
+    int heavy = 0;  // blocks moved to the front of the table
     int nslots = 0;
 };
 
@@ -306,16 +338,40 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
     }
     if (!any_split) out.vdest.clear();
     const int64_t nv = (int64_t)out.vrow_ptr.size() - 1;
-    out.blk.push_back(0);
+    std::vector<int2> order;  // blocks in row order
+    std::vector<int32_t> longest;
     int64_t start = 0;
-    for (int64_t v = 0; v < nv; ++v) {
-        const int64_t len = (int64_t)out.vrow_ptr[v + 1] - out.vrow_ptr[v];
-        if (v > start && (v - start >= CAP_ROWS || (int64_t)out.vrow_ptr[v] - out.vrow_ptr[start] + len > cap)) {
-            out.blk.push_back((int32_t)v);
+    int32_t lmax = 0;
+    for (int64_t v = 0; v <= nv; ++v) {
+        const int64_t len = v < nv ? (int64_t)out.vrow_ptr[v + 1] - out.vrow_ptr[v] : 0;
+        if (v == nv || (v > start && (v - start >= CAP_ROWS || (int64_t)out.vrow_ptr[v] - out.vrow_ptr[start] + len > cap))) {
+            if (v > start) {
+                order.push_back(make_int2((int)start, (int)v));
+                longest.push_back(lmax);
+            }
             start = v;
+            lmax = 0;
         }
+        lmax = std::max<int32_t>(lmax, (int32_t)len);
     }
-    if (nv > 0) out.blk.push_back((int32_t)nv);
+    // Longest-first for blocks whose longest row is a long serial chain (>= 256 nonzeros and >= 8x the mean row):
+    // they are dispatched first and overlap the rest of the grid.  Everything else keeps row order, so all XCDs
+    // sweep the same B window together.
+    const double mean = nv > 0 ? (double)(out.vrow_ptr[nv] - out.vrow_ptr[0]) / (double)nv : 0.0;
+#ifdef SPMM_EXP_NO_HEAVY_FIRST
+    const int32_t heavy_len = 1 << 30;
+#else
+    const int32_t heavy_len = (int32_t)std::max(256.0, 8.0 * mean);
+#endif
+    std::vector<int> hv;
+    for (size_t b = 0; b < order.size(); ++b)
+        if (longest[b] >= heavy_len) hv.push_back((int)b);
+    std::stable_sort(hv.begin(), hv.end(), [&](int a, int b) { return longest[a] > longest[b]; });
+    out.heavy = (int)hv.size();
+    out.blk.reserve(order.size());
+    for (int b : hv) out.blk.push_back(order[b]);
+    for (size_t b = 0; b < order.size(); ++b)
+        if (longest[b] < heavy_len) out.blk.push_back(order[b]);
 }
 
 }  // namespace
@@ -460,32 +516,35 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
 
     Plan pl;
     pl.k = k;
-    // K panels sized for the Infinity Cache
-    const int64_t panel_bytes = h->var.panel_bytes > 0 ? h->var.panel_bytes
-                                                        : (int64_t)env_int("SPMM_HIP_PANEL_MB", 192) * (1 << 20);
-    const int min_kw = std::max(1, (int)(16 / h->vsize));
+    // K panels of PANEL_ROW_BYTES-byte B rows when B would crowd the Infinity Cache and the B gather dominates the
+    // launch (>= 16 nonzeros per row); each extra panel re-streams A and cuts C rows into 256-B pieces, which only
+    // pays when it turns Infinity-Cache misses into hits (measured §6.2: config 2 K=128 1.65 ms at 32 columns vs
+    // 2.30 ms unpanelled; a 200 K-row, 10 nnz/row matrix with a 208 MB B is faster unpanelled).
+    const int panel_env = env_int("SPMM_HIP_PANEL_K", 0);
+    const double b_bytes = (double)h->ncols * k * (double)h->vsize;
+    const double avg_row = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
     pl.kw = k;
-    if ((int64_t)h->ncols * k * (int64_t)h->vsize > panel_bytes && k > min_kw) {
-        const int64_t fit = panel_bytes / std::max<int64_t>(1, h->ncols * (int64_t)h->vsize);
-        pl.kw = std::max(min_kw, pow2_floor(std::max<int64_t>(fit, 1)));
-        if (pl.kw >= k) pl.kw = k;
+    if (h->var.panel_k > 0 || panel_env > 0) {
+        pl.kw = std::min(k, h->var.panel_k > 0 ? h->var.panel_k : panel_env);
+    } else if (b_bytes > PANEL_MIN_B_BYTES && avg_row >= PANEL_MIN_ROW_NNZ) {
+        pl.kw = std::min(k, std::max(1, (int)(PANEL_ROW_BYTES / h->vsize)));
     }
     pl.npanels = (k + pl.kw - 1) / pl.kw;
     // block capacity and split length
     int vec, g;
     lane_layout(pl.kw, k, h->vsize, vec, g);
-    const int ng = WG / g;
-    pl.cap = h->var.cap > 0 ? h->var.cap : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
+    // block capacity: the LDS window (CAP), smaller for small matrices so >= ~1024 blocks exist (a 4096-nonzero
+    // window for one-lane row groups measured slower at K = 1, §6.2)
+    pl.cap = h->var.cap > 0 ? std::min(h->var.cap, CAP) : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
     const int seq_env = env_int("SPMM_HIP_SEQ_MAX", 0);
-    pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max
-                 : seq_env > 0      ? seq_env
-                                    : std::max(16, pl.cap / ng);
-    pl.seq_max = std::min(pl.seq_max, pl.cap);
+    pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max : seq_env > 0 ? seq_env : split_length(h, pl.kw);
+    pl.seq_max = std::max(1, std::min(pl.seq_max, CAP));
+    pl.cap = std::max(pl.cap, std::min(CAP, pow2_ceil(pl.seq_max)));   // a row of T nonzeros fits one block
 
     Inspection in;
     inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in);
     h->nv = (int64_t)in.vrow_ptr.size() - 1;
-    h->nblk = std::max(0, (int)in.blk.size() - 1);
+    h->nblk = (int)in.blk.size();
     h->nlong = (int)in.long_rows.size();
     h->nslots = in.nslots;
     h->plan = pl;
@@ -496,11 +555,12 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         return e;
     };
     hipError_t e = alloc_copy((void **)&h->d_vrow_ptr, in.vrow_ptr.data(), in.vrow_ptr.size() * 4);
-    if (e == hipSuccess) e = alloc_copy((void **)&h->d_blk, in.blk.data(), in.blk.size() * 4);
+    if (e == hipSuccess) e = alloc_copy((void **)&h->d_blk, in.blk.data(), in.blk.size() * sizeof(int2));
     if (e == hipSuccess && !in.vdest.empty()) e = alloc_copy((void **)&h->d_vdest, in.vdest.data(), in.vdest.size() * 4);
     if (e == hipSuccess && h->nlong > 0)
         e = alloc_copy((void **)&h->d_long_rows, in.long_rows.data(), in.long_rows.size() * sizeof(int4));
-    h->insp_bytes = (in.vrow_ptr.size() + in.blk.size() + in.vdest.size()) * 4 + in.long_rows.size() * sizeof(int4);
+    h->insp_bytes = (in.vrow_ptr.size() + in.vdest.size()) * 4 + in.blk.size() * sizeof(int2) +
+                    in.long_rows.size() * sizeof(int4);
     h->b_bytes = (size_t)std::max<int64_t>(h->ncols, 1) * k * h->vsize;
     h->c_bytes = (size_t)std::max<int64_t>(h->m, 1) * k * h->vsize;
     if (e == hipSuccess) e = hipMalloc(&h->d_b, h->b_bytes);
@@ -666,16 +726,16 @@ int spmm_hip_destroy(spmm_hip_t *h) {
 
 #ifdef SPMM_TUNING
 // Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): kernel variant + inspector overrides; the
-// next run re-plans.  0 = policy default for seq_max / cap / panel_mb.
-int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int remap, int buf, int seq_max, int cap, int panel_mb) {
+// next run re-plans.  0 = policy default for seq_max / cap / panel_k.
+int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int seq_max, int cap, int panel_k) {
     if (!h) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
     h->var.u = u;
     h->var.ntc = ntc;
-    h->var.remap = remap;
+    h->var.dma = dma;
     h->var.buf = buf;
     h->var.seq_max = seq_max;
     h->var.cap = cap;
-    h->var.panel_bytes = (int64_t)panel_mb * (1 << 20);
+    h->var.panel_k = panel_k;
     const int k = h->plan.k;
     h->plan.k = -1;
     return k > 0 ? spmm_hip_plan(h, k) : SPMM_HIP_OK;

@@ -7,7 +7,7 @@
 //   * The inspector (spmm_engine.hip) turns A's rows into VIRTUAL ROWS of at most T nonzeros (a row longer than T
 //     becomes ceil(len/T) consecutive pieces) and packs consecutive virtual rows into nnz-balanced BLOCKS.
 //   * One workgroup (256 lanes = 4 wave64) per block: the block's col_idx / values / row offsets are staged into
-//     LDS by LDS-DMA (global_load_lds, 16-byte lanes); a ROW GROUP of G lanes owns one virtual row; each lane owns VEC consecutive
+//     LDS (16-byte lanes); a ROW GROUP of G lanes owns one virtual row; each lane owns VEC consecutive
 //     columns of the K-panel (16-byte gathers of the row-major B row), issues U gathers, then accumulates them in
 //     CSR order with one FMA each -- the same left-to-right fused chain as the reference built with its own flags,
 //     so every row that is not split is bit-identical to the reference.
@@ -23,7 +23,6 @@ namespace spmm {
 
 constexpr int WG = 256;          // lanes per workgroup (4 wavefronts)
 constexpr int CAP_ROWS = 512;    // virtual rows per block
-constexpr int NXCD = 8;          // MI355X: 8 accelerator dies, one L2 each
 
 template <typename T, int N>
 struct alignas(sizeof(T) * N) vec {
@@ -88,12 +87,6 @@ struct BGather {
 
 // Bijective XCD-aware remap (optional): hardware deals workgroups round-robin over the 8 XCDs, this gives each
 // XCD a contiguous run of blocks.  Speed only; any placement gives the same result.
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-    const int q = nblk / NXCD, r = nblk % NXCD;
-    const int x = bid % NXCD, i = bid / NXCD;
-    return x * q + (x < r ? x : r) + i;
-}
-
 // One virtual row, nonzeros [a, e) of the LDS-staged block: U gathers in flight, then U FMAs in CSR order.
 template <typename T, int VEC, int U, typename Gather>
 __device__ __forceinline__ vec<T, VEC> row_dot(const int32_t *s_col, const T *s_val, int a, int e,
@@ -121,15 +114,16 @@ __device__ __forceinline__ vec<T, VEC> row_dot(const int32_t *s_col, const T *s_
 }
 
 // ------------------------------------------------------------------------------------------------ row blocks
-// blk[b] .. blk[b+1]: the virtual rows of block b (<= CAP nonzeros in all, <= CAP_ROWS rows).  vrow_ptr indexes
+// blk[b] = {first, end}: the virtual rows of block b (<= CAP nonzeros in all, <= CAP_ROWS rows); blocks holding
+// long serial rows come first in the table (they start at time 0), the rest in row order.  vrow_ptr indexes
 // the original col_idx / values.  SPLIT: vdest[v] >= 0 is v's C row, < 0 is partial slot -vdest[v]-1; otherwise
 // virtual row v IS C row v.  B and C point at the panel's first column; ld is their row stride (K); kw the panel
 // width.
-template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool REMAP, bool BUF, bool SPLIT>
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, bool SPLIT>
 __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
-                                                       const int32_t *__restrict__ blk, int nblk,
+                                                       const int2 *__restrict__ blk, int nblk,
                                                        const int32_t *__restrict__ vdest,
                                                        const T *__restrict__ B, T *__restrict__ C, T *__restrict__ P,
                                                        int ld, int kw, uint32_t b_bytes) {
@@ -141,20 +135,21 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     using V = vec<T, VEC>;
     constexpr int NG = WG / G;
 
-    const int b = REMAP ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
+    const int b = (int)blockIdx.x;
     const int tid = threadIdx.x;
-    const int r0 = blk[b], r1 = blk[b + 1];
+    const int2 rr = blk[b];
+    const int r0 = rr.x, r1 = rr.y;
     const int nrows = r1 - r0;
     const int j0 = vrow_ptr[r0];
     const int j1 = vrow_ptr[r1];
 
-    // Stage the block by LDS-DMA (global_load_lds: no VGPR destinations, all issued before the barrier's wait):
-    // col_idx / values in 1-KiB wave pieces of 16-byte lanes from the 16-byte boundary jb <= j0 (the device arrays
-    // are padded), the virtual-row offsets in 256-B pieces of 4-byte lanes.
-    typedef __attribute__((address_space(3))) void lds_void;
+    // Stage the block (col_idx / values from the 16-byte boundary jb <= j0 -- the device arrays are padded -- and the
+    // virtual-row offsets).  DMA: LDS-DMA (global_load_lds, no VGPR destinations) in 1-KiB wave pieces of 16-byte
+    // lanes; otherwise 16-byte non-temporal vector loads through VGPRs and ds_write.
     const int jb = j0 & ~3;
     const int cnt = j1 - jb;
-    {
+    if constexpr (DMA) {
+        typedef __attribute__((address_space(3))) void lds_void;
         const int wave = tid / 64, wl = tid % 64;
         const int ncp = (cnt + 255) / 256;                        // 256 int32 per KiB piece
         for (int q = wave; q < ncp; q += WG / 64) {
@@ -172,6 +167,36 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
             const int i = q * 64 + wl;
             if (i <= nrows) __builtin_amdgcn_global_load_lds((const void *)(vrow_ptr + r0 + i), (lds_void *)(s_rp + q * 64), 4, 0, 0);
         }
+    } else {
+        // every load of the block issued into VGPRs before the first LDS write: one memory round trip per block
+        typedef T tv __attribute__((ext_vector_type(SVN)));
+        constexpr int NC = (CAPP / 4 + WG - 1) / WG;
+        constexpr int NV = (CAPP / SVN + WG - 1) / WG;
+        constexpr int NR = (CAP_ROWS + 1 + WG - 1) / WG;
+        const int nc = (cnt + 3) / 4, nv = (cnt + SVN - 1) / SVN;
+        i32x4 cb[NC];
+        tv vb[NV];
+        int rp[NR];
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+            if (tid + u * WG < nc)
+                cb[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(col_idx + jb) + tid + u * WG);
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+            if (tid + u * WG < nv)
+                vb[u] = __builtin_nontemporal_load(reinterpret_cast<const tv *>(vals + jb) + tid + u * WG);
+#pragma unroll
+        for (int u = 0; u < NR; ++u)
+            if (tid + u * WG <= nrows) rp[u] = vrow_ptr[r0 + tid + u * WG];
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+            if (tid + u * WG < nc) reinterpret_cast<i32x4 *>(s_col)[tid + u * WG] = cb[u];
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+            if (tid + u * WG < nv) reinterpret_cast<tv *>(s_val)[tid + u * WG] = vb[u];
+#pragma unroll
+        for (int u = 0; u < NR; ++u)
+            if (tid + u * WG <= nrows) s_rp[tid + u * WG] = rp[u];
     }
     __syncthreads();
 
@@ -195,10 +220,39 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     }
 }
 
-// long_rows[i] = {row, first_slot, nslots, 0}: C[row][n] = sum of the row's partial slots, in slot order.
+// long_rows[b] = {row, first_slot, nslots, 0}: C[row][n] = sum of the row's partial slots P[first_slot + q][n].
+// One workgroup per split row: KW = min(pow2ceil(K), 64) columns per pass x SL = 256/KW slot lanes; slot lane l sums
+// slots l, l+SL, ... in order, then a fixed binary tree over the slot lanes in LDS (deterministic: the shape depends
+// only on nslots and K; O(nslots/SL + log SL) deep instead of a serial chain over all slots).
 template <typename T>
-__global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict__ long_rows, int nlong,
+__global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict__ long_rows,
                                                           const T *__restrict__ P, T *__restrict__ C, int K) {
+    __shared__ T red[WG];
+    const int4 lr = long_rows[blockIdx.x];
+    int kw = 1;
+    while (kw < K && kw < 64) kw <<= 1;
+    const int sl_n = WG / kw;
+    const int n = threadIdx.x % kw, sl = threadIdx.x / kw;
+    for (int c0 = 0; c0 < K; c0 += kw) {
+        const int col = c0 + n;
+        T s = T(0);
+        if (col < K)
+            for (int q = sl; q < lr.z; q += sl_n) s += P[(size_t)(lr.y + q) * K + col];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = sl_n / 2; w >= 1; w /= 2) {
+            if (sl < w) red[threadIdx.x] += red[threadIdx.x + w * kw];
+            __syncthreads();
+        }
+        if (sl == 0 && col < K) C[(size_t)lr.x * K + col] = red[n];
+        __syncthreads();
+    }
+}
+
+#ifdef SPMM_EXP_SERIAL_COMBINE
+template <typename T>
+__global__ __launch_bounds__(WG) void spmm_combine_serial_kernel(const int4 *__restrict__ long_rows, int nlong,
+                                                                 const T *__restrict__ P, T *__restrict__ C, int K) {
     const int64_t t = (int64_t)blockIdx.x * WG + threadIdx.x;
     if (t >= (int64_t)nlong * K) return;
     const int li = (int)(t / K), n = (int)(t % K);
@@ -207,6 +261,7 @@ __global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict
     for (int q = 1; q < lr.z; ++q) s += P[(size_t)(lr.y + q) * K + n];
     C[(size_t)lr.x * K + n] = s;
 }
+#endif
 
 // ------------------------------------------------------------------------------------------------ transpose
 // Reference B layout (column-major, x[n*ncols + c]) -> engine layout (row-major, B[c*K + n]).

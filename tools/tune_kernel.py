@@ -18,12 +18,12 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 
-# (U, NTC, REMAP, BUF, seq_max, cap, panel_mb): 0 = inspector policy default
-VARIANTS = [(16, 1, 0, 0, 0, 0, 0), (16, 1, 0, 0, 2048, 2048, 0), (8, 1, 0, 0, 0, 0, 0), (24, 1, 0, 0, 0, 0, 0),
-            (16, 1, 0, 1, 0, 0, 0), (16, 1, 0, 0, 64, 0, 0), (16, 1, 0, 0, 32, 0, 0), (16, 1, 0, 0, 0, 1024, 0),
-            (16, 1, 0, 0, 0, 512, 0), (16, 1, 0, 0, 0, 0, 96), (16, 1, 0, 0, 0, 0, 128), (16, 1, 0, 0, 0, 0, 256),
-            (16, 1, 0, 0, 0, 0, 512), (16, 1, 0, 0, 0, 0, 4096)]
-FIELDS = ("U", "NTC", "REMAP", "BUF", "SEQ_MAX", "CAP", "PANEL_MB")
+# (U, NTC, DMA, BUF, seq_max, cap, panel_k): 0 = inspector policy default
+VARIANTS = [(16, 1, 0, 1, 0, 0, 0), (16, 1, 1, 1, 0, 0, 0), (16, 1, 0, 0, 0, 0, 0), (8, 1, 0, 1, 0, 0, 0),
+            (16, 1, 0, 1, 2048, 0, 0), (16, 1, 0, 1, 64, 0, 0), (16, 1, 0, 1, 128, 0, 0), (16, 1, 0, 1, 256, 0, 0),
+            (16, 1, 0, 1, 512, 0, 0), (16, 1, 0, 1, 0, 1024, 0), (16, 1, 0, 1, 0, 2048, 0), (16, 1, 0, 1, 0, 4096, 0),
+            (16, 1, 0, 1, 0, 0, 16), (16, 1, 0, 1, 0, 0, 64), (16, 1, 0, 1, 0, 0, 4096)]
+FIELDS = ("U", "NTC", "DMA", "BUF", "SEQ_MAX", "CAP", "PANEL_K")
 
 
 def main():
@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="comma list of variant indices")
+    ap.add_argument("--variants", default="", help="';'-separated U,NTC,DMA,BUF,SEQ_MAX,CAP,PANEL_K tuples")
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     args = ap.parse_args()
 
@@ -58,6 +59,8 @@ def main():
     sp = C.c_void_p(stream.cuda_stream)
 
     variants = VARIANTS if not args.only else [VARIANTS[int(i)] for i in args.only.split(",")]
+    if args.variants:
+        variants = [tuple(int(x) for x in v.split(",")) for v in args.variants.split(";")]
     bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if args.dtype == "f64" else S.F32)
     ref = None
     res = {v: [] for v in variants}
@@ -77,9 +80,9 @@ def main():
             torch.cuda.synchronize()
             res[v].append(e0.elapsed_time(e1) / args.iters)
             if rnd == 0:
-                inf = (C.c_int64 * 12)()
+                inf = np.zeros(12, np.int64)
                 T.spmm_hip_info(h, inf)
-                plan[v] = {"T": inf[8], "cap": inf[9], "panel_k": inf[10], "blocks": inf[5], "split_rows": inf[6]}
+                plan[v] = {"T": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]), "blocks": int(inf[5]), "split_rows": int(inf[6])}
                 out = Cm.clone()
                 if ref is None:
                     ref = out
