@@ -248,12 +248,7 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         }
     }
     if (h->nlong > 0) {
-#ifdef SPMM_EXP_SERIAL_COMBINE
-        const int64_t tot = (int64_t)h->nlong * K;
-        spmm_combine_serial_kernel<T><<<(unsigned)((tot + WG - 1) / WG), WG, 0, s>>>(h->d_long_rows, h->nlong, P, C, K);
-#else
         spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
-#endif
     }
 }
 
@@ -358,11 +353,7 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
     // they are dispatched first and overlap the rest of the grid.  Everything else keeps row order, so all XCDs
     // sweep the same B window together.
     const double mean = nv > 0 ? (double)(out.vrow_ptr[nv] - out.vrow_ptr[0]) / (double)nv : 0.0;
-#ifdef SPMM_EXP_NO_HEAVY_FIRST
-    const int32_t heavy_len = 1 << 30;
-#else
     const int32_t heavy_len = (int32_t)std::max(256.0, 8.0 * mean);
-#endif
     std::vector<int> hv;
     for (size_t b = 0; b < order.size(); ++b)
         if (longest[b] >= heavy_len) hv.push_back((int)b);

@@ -249,19 +249,6 @@ __global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict
     }
 }
 
-#ifdef SPMM_EXP_SERIAL_COMBINE
-template <typename T>
-__global__ __launch_bounds__(WG) void spmm_combine_serial_kernel(const int4 *__restrict__ long_rows, int nlong,
-                                                                 const T *__restrict__ P, T *__restrict__ C, int K) {
-    const int64_t t = (int64_t)blockIdx.x * WG + threadIdx.x;
-    if (t >= (int64_t)nlong * K) return;
-    const int li = (int)(t / K), n = (int)(t % K);
-    const int4 lr = long_rows[li];
-    T s = P[(size_t)lr.y * K + n];
-    for (int q = 1; q < lr.z; ++q) s += P[(size_t)(lr.y + q) * K + n];
-    C[(size_t)lr.x * K + n] = s;
-}
-#endif
 
 // ------------------------------------------------------------------------------------------------ transpose
 // Reference B layout (column-major, x[n*ncols + c]) -> engine layout (row-major, B[c*K + n]).

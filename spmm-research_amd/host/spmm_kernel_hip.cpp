@@ -61,7 +61,7 @@ struct Matrix_Format *csr_to_format(INT_T *row_ptr, INT_T *col_ind, ValueType *v
     const char *dev = getenv("SPMM_HIP_DEVICE");
     int st = spmm_hip_create(row_ptr, col_ind, values, m, n, nnz, k, kDtype, dev ? atoi(dev) : 0, &csr->h);
     if (st != SPMM_HIP_OK) die("csr_to_format", st);
-    int64_t info[8];
+    int64_t info[SPMM_HIP_INFO_SLOTS];
     spmm_hip_info(csr->h, info);
     csr->mem_footprint = (double)info[7];
     return csr;
