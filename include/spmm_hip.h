@@ -89,15 +89,19 @@ int spmm_hip_last_times(spmm_hip_t *h, double *out_ms);
  * (spmv_kernel.h:20,30; spmv_bench.cpp:441-443,474-476).  Appends CSV columns to buf (at most buf_n bytes incl.
  * NUL) and returns the number of characters written (<0 on error).  Columns:
  *   kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,split_rows,seq_max,panels,
- *   device */
+ *   windows,device */
 int spmm_hip_stats_labels(char *buf, long buf_n);
 int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
 
-#define SPMM_HIP_INFO_SLOTS 12
+#define SPMM_HIP_INFO_SLOTS 16
 
-/* Properties of the handle (out has SPMM_HIP_INFO_SLOTS = 12 slots): out[0]=m, out[1]=ncols, out[2]=nnz, out[3]=k planned, out[4]=dtype,
- * out[5]=workgroup blocks, out[6]=split rows, out[7]=device bytes held, out[8]=split length T (rows with <= T
- * nonzeros are bit-exact), out[9]=block capacity, out[10]=K-panel width, out[11]=K panels. */
+/* Properties of the handle (out has SPMM_HIP_INFO_SLOTS = 16 slots): out[0]=m, out[1]=ncols, out[2]=nnz,
+ * out[3]=k planned, out[4]=dtype, out[5]=workgroup blocks, out[6]=split rows, out[7]=device bytes held,
+ * out[8]=split length T (rows with <= T nonzeros are bit-exact), out[9]=block capacity, out[10]=K-panel width,
+ * out[11]=K panels, out[12]=column windows (1 = none; > 1: one launch per window, each row's FMA chain continued
+ * through C from window to window, still bit-exact -- SPMM_HIP_WIN_BYTES=<bytes of B per window> forces them,
+ * -1 disables), out[13]=window width in columns (0 = none), out[14]=virtual rows (row segments) over all windows,
+ * out[15]=reserved (0). */
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
 
 /* Device buffers owned by the handle (for callers that stage B/C themselves), row-major B of the planned k. */
@@ -113,6 +117,25 @@ int spmm_hip_partition_rows(const int32_t *row_ptr, int64_t m, int64_t nnz, int6
 /* Algorithmic byte model per SpMM call (reference SpMV model spmv_operator.cu:30-32 extended to
  * K columns): 4(m+1) + (4+s)nnz + s*K*ncols + s*K*m, s = sizeof(value). */
 double spmm_hip_bytes_alg(int64_t m, int64_t ncols, int64_t nnz, int32_t k, int32_t dtype);
+
+/* Diagnostics (host only, no device needed): the inspector's work decomposition for a CSR pattern, for tests.
+ * win_cols = 0: one window (the plain row split); > 0: column windows of that many columns (chained mode; every
+ * row's columns must be sorted).  On success the arrays are malloc'ed; release with spmm_hip_debug_free.
+ *   vrow_ptr[nv+1]   virtual-row offsets into the (window-major, if windowed) nonzero order
+ *   vdest[nv]        destination code (0-length if no row is split and there are no windows): plain split mode
+ *                    d (C row >= 0, slot -s-1); windowed mode (d << 1) | continue
+ *   blk[2*nblk]      {first, end} virtual rows of each workgroup block
+ *   win_blk[nwin+1]  blocks of window w: [win_blk[w], win_blk[w+1])
+ *   perm[nz]         windowed mode: original nonzero index of each position (NULL otherwise)
+ *   long_rows[4*nlong] {row, first slot, slots, 0} of each split row */
+typedef struct {
+    int64_t nv, nblk, nwin, nz, nlong, nslots;
+    int32_t *vrow_ptr, *vdest, *blk, *win_blk, *long_rows;
+    int64_t *perm;
+} spmm_hip_inspection_t;
+int spmm_hip_debug_inspect(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
+                           int32_t cap, int64_t win_cols, spmm_hip_inspection_t *out);
+void spmm_hip_debug_free(spmm_hip_inspection_t *ins);
 
 const char *spmm_hip_strerror(int status);
 const char *spmm_hip_last_error_detail(void);

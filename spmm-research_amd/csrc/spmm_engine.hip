@@ -72,12 +72,16 @@ struct Plan {
     int kw = 0, npanels = 0;   // panel width (columns) and count
     int seq_max = 0;           // T
     int cap = 0;               // block capacity (nonzeros)
+    int64_t win_cols = 0;      // column-window width (0 = one window over all columns)
+    int nwin = 1;              // column windows (one launch each per K panel)
+    int64_t nseg = 0;          // virtual rows (segments) over all windows
 };
 
 struct Variant {
     int u = DEF_U, ntc = DEF_NTC, dma = DEF_DMA, buf = DEF_BUF;
     int seq_max = 0, cap = 0;  // 0 = inspector policy
     int panel_k = 0;           // 0 = inspector policy
+    int64_t win_bytes = 0;     // 0 = inspector policy, < 0 = no column windows, > 0 = window of this many B bytes
 };
 
 }  // namespace
@@ -100,6 +104,9 @@ struct spmm_hip_handle {
     int32_t *d_vrow_ptr = nullptr, *d_vdest = nullptr;
     int2 *d_blk = nullptr;
     int4 *d_long_rows = nullptr;
+    std::vector<int> win_blk;        // blocks of column window w: [win_blk[w], win_blk[w+1])
+    int32_t *d_wcol = nullptr;       // chained mode: col_idx / values in window-major segment order
+    void *d_wval = nullptr;
 
     // per-k buffers
     void *d_b = nullptr;      // row-major B [ncols][k]
@@ -143,10 +150,14 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 }
 
 void free_plan(spmm_hip_t *h) {
-    void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows};
+    void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
+                  h->d_wcol, h->d_wval};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
+    h->d_wcol = nullptr;
+    h->d_wval = nullptr;
+    h->win_blk.clear();
     h->d_vrow_ptr = h->d_vdest = nullptr;
     h->d_blk = nullptr;
     h->d_long_rows = nullptr;
@@ -160,14 +171,24 @@ void free_plan(spmm_hip_t *h) {
 template <typename T, int VEC, int G, int U, bool NTC, bool DMA, bool BUF>
 void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
     const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * ld * sizeof(T), 0xFFFFFFFFull);
-    auto go = [&](auto split_c) {
-        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(split_c)::value><<<h->nblk, WG, 0, s>>>(
+    if (h->plan.nwin > 1) {
+        // chained mode: one launch per column window, in window order (each continues the chains of the last)
+        for (int w = 0; w < h->plan.nwin; ++w) {
+            const int b0 = h->win_blk[w], nb = h->win_blk[w + 1] - b0;
+            if (nb == 0) continue;
+            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, DEST_CHAIN><<<nb, WG, 0, s>>>(
+                h->d_vrow_ptr, h->d_wcol, (const T *)h->d_wval, h->d_blk + b0, nb, h->d_vdest, B, C, P, ld, kw, bb);
+        }
+        return;
+    }
+    auto go = [&](auto mode_c) {
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value><<<h->nblk, WG, 0, s>>>(
             h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
     };
     if (h->nslots > 0)
-        go(std::true_type());
+        go(std::integral_constant<int, DEST_SPLIT>());
     else
-        go(std::false_type());
+        go(std::integral_constant<int, DEST_ROW>());
 }
 
 // 32-bit buffer offsets for the B gather are valid while B fits 4 GiB.
@@ -300,18 +321,48 @@ struct Inspection {
     std::vector<int32_t> vrow_ptr, vdest;
     std::vector<int2> blk;
     std::vector<int4> long_rows;
+    std::vector<int> win_blk;       // chained mode: block offsets per window
+    std::vector<int64_t> perm;      // chained mode: position in the window-major arrays -> original nonzero
     int heavy = 0;  // blocks moved to the front of the table
     int nslots = 0;
 };
 
-// Virtual rows (rows longer than T cut into T-nonzero pieces) packed greedily into blocks of <= cap nonzeros and
-// <= CAP_ROWS virtual rows.
+// Pack virtual rows [v0, v1) greedily into blocks of <= cap nonzeros and <= CAP_ROWS virtual rows, appended to out.
+// Longest-first for blocks whose longest row is a long serial chain (>= 256 nonzeros and >= 8x the mean row):
+// they are dispatched first and overlap the rest of the grid.  Everything else keeps row order, so all XCDs
+// sweep the same B window together.
+void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap, Inspection &out) {
+    std::vector<int2> order;
+    std::vector<int32_t> longest;
+    int64_t start = v0;
+    int32_t lmax = 0;
+    for (int64_t v = v0; v <= v1; ++v) {
+        const int64_t len = v < v1 ? (int64_t)vp[v + 1] - vp[v] : 0;
+        if (v == v1 || (v > start && (v - start >= CAP_ROWS || (int64_t)vp[v] - vp[start] + len > cap))) {
+            if (v > start) {
+                order.push_back(make_int2((int)start, (int)v));
+                longest.push_back(lmax);
+            }
+            start = v;
+            lmax = 0;
+        }
+        lmax = std::max<int32_t>(lmax, (int32_t)len);
+    }
+    const double mean = v1 > v0 ? (double)(vp[v1] - vp[v0]) / (double)(v1 - v0) : 0.0;
+    const int32_t heavy_len = (int32_t)std::max(256.0, 8.0 * mean);
+    std::vector<int> hv;
+    for (size_t b = 0; b < order.size(); ++b)
+        if (longest[b] >= heavy_len) hv.push_back((int)b);
+    std::stable_sort(hv.begin(), hv.end(), [&](int a, int b) { return longest[a] > longest[b]; });
+    out.heavy += (int)hv.size();
+    for (int b : hv) out.blk.push_back(order[b]);
+    for (size_t b = 0; b < order.size(); ++b)
+        if (longest[b] < heavy_len) out.blk.push_back(order[b]);
+}
+
+// Virtual rows (rows longer than T cut into T-nonzero pieces) packed into blocks (one column window).
 void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
-    out.vrow_ptr.clear();
-    out.vdest.clear();
-    out.blk.clear();
-    out.long_rows.clear();
-    out.nslots = 0;
+    out = Inspection();
     out.vrow_ptr.reserve((size_t)m + 1);
     out.vrow_ptr.push_back(rp[0]);
     bool any_split = false;
@@ -332,37 +383,170 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
         }
     }
     if (!any_split) out.vdest.clear();
-    const int64_t nv = (int64_t)out.vrow_ptr.size() - 1;
-    std::vector<int2> order;  // blocks in row order
-    std::vector<int32_t> longest;
-    int64_t start = 0;
-    int32_t lmax = 0;
-    for (int64_t v = 0; v <= nv; ++v) {
-        const int64_t len = v < nv ? (int64_t)out.vrow_ptr[v + 1] - out.vrow_ptr[v] : 0;
-        if (v == nv || (v > start && (v - start >= CAP_ROWS || (int64_t)out.vrow_ptr[v] - out.vrow_ptr[start] + len > cap))) {
-            if (v > start) {
-                order.push_back(make_int2((int)start, (int)v));
-                longest.push_back(lmax);
-            }
-            start = v;
-            lmax = 0;
+    pack_blocks(out.vrow_ptr, 0, (int64_t)out.vrow_ptr.size() - 1, cap, out);
+}
+
+// Every row's columns non-decreasing (coo_to_csr's output).  Column windows keep each row's CSR order only then.
+bool rows_sorted(const int32_t *rp, const int32_t *col, int64_t m) {
+    for (int64_t r = 0; r < m; ++r)
+        for (int64_t j = (int64_t)rp[r] + 1; j < rp[r + 1]; ++j)
+            if (col[j] < col[j - 1]) return false;
+    return true;
+}
+
+// Pieces of the row split (rows <= T whole, longer rows in T-nonzero pieces to partial slots), in row order:
+// {destination (C row >= 0, slot -s-1), first nonzero, end}.
+struct Piece {
+    int32_t d;
+    int32_t s, e;
+};
+void make_pieces(const int32_t *rp, int64_t m, int T, std::vector<Piece> &pcs, Inspection &out) {
+    pcs.clear();
+    pcs.reserve((size_t)m);
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t len = (int64_t)rp[r + 1] - rp[r];
+        if (len <= T) {
+            pcs.push_back({(int32_t)r, rp[r], rp[r + 1]});
+        } else {
+            const int pieces = (int)((len + T - 1) / T);
+            out.long_rows.push_back(make_int4((int)r, out.nslots, pieces, 0));
+            for (int q = 0; q < pieces; ++q)
+                pcs.push_back({-(out.nslots + q) - 1, (int32_t)(rp[r] + (int64_t)q * T),
+                               (int32_t)std::min<int64_t>((int64_t)rp[r] + (int64_t)(q + 1) * T, rp[r + 1])});
+            out.nslots += pieces;
         }
-        lmax = std::max<int32_t>(lmax, (int32_t)len);
     }
-    // Longest-first for blocks whose longest row is a long serial chain (>= 256 nonzeros and >= 8x the mean row):
-    // they are dispatched first and overlap the rest of the grid.  Everything else keeps row order, so all XCDs
-    // sweep the same B window together.
-    const double mean = nv > 0 ? (double)(out.vrow_ptr[nv] - out.vrow_ptr[0]) / (double)nv : 0.0;
-    const int32_t heavy_len = (int32_t)std::max(256.0, 8.0 * mean);
-    std::vector<int> hv;
-    for (size_t b = 0; b < order.size(); ++b)
-        if (longest[b] >= heavy_len) hv.push_back((int)b);
-    std::stable_sort(hv.begin(), hv.end(), [&](int a, int b) { return longest[a] > longest[b]; });
-    out.heavy = (int)hv.size();
-    out.blk.reserve(order.size());
-    for (int b : hv) out.blk.push_back(order[b]);
-    for (size_t b = 0; b < order.size(); ++b)
-        if (longest[b] < heavy_len) out.blk.push_back(order[b]);
+}
+
+// Segments a piece would make with windows of W columns (the window index changes along the sorted row).
+int64_t count_segments(const std::vector<Piece> &pcs, const int32_t *col, int64_t W) {
+    int64_t n = 0;
+    for (const Piece &p : pcs) {
+        if (p.s == p.e) {
+            ++n;
+            continue;
+        }
+        int64_t last = -1;
+        for (int32_t j = p.s; j < p.e; ++j) {
+            const int64_t w = col[j] / W;
+            n += (w != last);
+            last = w;
+        }
+    }
+    return n;
+}
+
+// Chained mode (column windows of W columns): every piece is cut where its column window changes; window w's
+// segments form the virtual rows of launch w, in row order, their nonzeros copied window-major (perm).  A
+// segment's vdest is (d << 1) | cont, cont = 1 unless it is the piece's first segment (the chain continues from
+// the value the previous window stored).  Empty rows get one empty segment in window 0 (they store 0).
+void inspect_windows(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int cap, int64_t W,
+                     Inspection &out) {
+    out = Inspection();
+    std::vector<Piece> pcs;
+    make_pieces(rp, m, T, pcs, out);
+    const int nwin = (int)((ncols + W - 1) / W);
+    std::vector<int64_t> nseg_w(nwin + 1, 0), nnz_w(nwin + 1, 0);
+    for (const Piece &p : pcs) {
+        if (p.s == p.e) {
+            ++nseg_w[0];
+            continue;
+        }
+        int64_t last = -1;
+        for (int32_t j = p.s; j < p.e; ++j) {
+            const int64_t w = col[j] / W;
+            nseg_w[w] += (w != last);
+            ++nnz_w[w];
+            last = w;
+        }
+    }
+    std::vector<int64_t> seg_off(nwin + 1, 0), nz_off(nwin + 1, 0);
+    for (int w = 0; w < nwin; ++w) {
+        seg_off[w + 1] = seg_off[w] + nseg_w[w];
+        nz_off[w + 1] = nz_off[w] + nnz_w[w];
+    }
+    const int64_t nseg = seg_off[nwin];
+    out.vrow_ptr.assign((size_t)nseg + 1, 0);
+    out.vdest.assign((size_t)nseg, 0);
+    out.perm.assign((size_t)nz_off[nwin], 0);
+    std::vector<int64_t> sc(seg_off.begin(), seg_off.end() - 1), nc(nz_off.begin(), nz_off.end() - 1);
+    for (const Piece &p : pcs) {
+        if (p.s == p.e) {
+            const int64_t v = sc[0]++;
+            out.vdest[v] = p.d * 2;
+            out.vrow_ptr[v] = (int32_t)nc[0];
+            continue;
+        }
+        int64_t last = -1;
+        for (int32_t j = p.s; j < p.e; ++j) {
+            const int64_t w = col[j] / W;
+            if (w != last) {
+                const int64_t v = sc[w]++;
+                out.vdest[v] = p.d * 2 + (last >= 0 ? 1 : 0);
+                out.vrow_ptr[v] = (int32_t)nc[w];
+                last = w;
+            }
+            out.perm[nc[w]++] = j;
+        }
+    }
+    out.vrow_ptr[nseg] = (int32_t)nz_off[nwin];
+    out.win_blk.push_back(0);
+    for (int w = 0; w < nwin; ++w) {
+        pack_blocks(out.vrow_ptr, seg_off[w], seg_off[w + 1], cap, out);
+        out.win_blk.push_back((int)out.blk.size());
+    }
+}
+
+// Column-window policy (measured on MI355X; profiles/r01_windows_*.log).  A launch gathers one B row
+// (kw*s bytes, at least one 128-byte L2 line) per nonzero.  Processed in row order, consecutive rows sweep a band of
+// columns together, so the B lines in use at any moment are about one row span (max col - min col) wide: when the
+// span's lines fit an XCD's L2 (x = span lines / L2 < 1.5) the plain launch already gathers from L2 and windows only
+// add launches and C round trips (72 K rows, 500 nnz, x = 1.4: 0.58 -> 0.60..0.66 ms; 100 nnz/row, bw 0.05:
+// 0.18 -> 0.30 ms).  When the span is wider, windows that keep an L2-sized slice of B hot pay, provided a row's
+// piece of one window stays long (>= 48 nonzeros): 500 nnz/row matrices 1.12-1.49x at K=32 and 1.54-1.96x at K=8;
+// config 2 (20 nnz over a 300 K-column span: 9 nnz per segment) and 100 nnz/row, bw 0.3 (7-27) lose 1.3-2.5x, as does
+// K=1 (its 8-byte gathers are request-bound).  Returns the window width in columns, 0 = no windows.
+constexpr double WIN_L2_BYTES = 4.0 * (1 << 20);   // L2 per XCD
+constexpr double WIN_MIN_SPAN = 1.5;               // row-span lines >= this many L2s
+constexpr double WIN_MIN_SEG = 48.0;               // mean nonzeros per segment at the chosen width
+constexpr double WIN_MIN_ROW_BYTES = 32.0;         // B row bytes: K=1..3 fp64 gathers are request-bound
+constexpr double WIN_LINE = 128.0;                 // L2 line
+
+// Window width in B bytes for a B row of srow bytes (measured best: 1-1.5 MB at K=8 fp64, 4-6 MB at K=32/128 fp64).
+double window_bytes(double srow) {
+    return srow <= 64.0 ? 1.5 * (1 << 20) : srow <= 128.0 ? 3.0 * (1 << 20) : 6.0 * (1 << 20);
+}
+
+double mean_row_span(const int32_t *rp, const int32_t *col, int64_t m) {
+    double sum = 0.0;
+    int64_t n = 0;
+    for (int64_t r = 0; r < m; ++r)
+        if (rp[r + 1] > rp[r]) {
+            sum += (double)col[rp[r + 1] - 1] - (double)col[rp[r]] + 1.0;
+            ++n;
+        }
+    return n > 0 ? sum / (double)n : 0.0;
+}
+
+int64_t window_cols(const spmm_hip_t *h, int kw, const std::vector<Piece> &pcs, const int32_t *col,
+                    int64_t win_bytes_var, int64_t *nseg_out) {
+    *nseg_out = 0;
+    const double srow = (double)kw * (double)h->vsize;
+    const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
+    const int64_t forced = win_bytes_var != 0 ? win_bytes_var : env_bytes;
+    if (forced < 0 || h->nnz == 0 || h->ncols < 2) return 0;
+    const double wb = forced > 0 ? (double)forced : window_bytes(srow);
+    const int64_t W = std::max<int64_t>(1, (int64_t)(wb / srow));
+    if (W >= h->ncols) return 0;
+    if (forced == 0) {
+        if (srow < WIN_MIN_ROW_BYTES) return 0;
+        if (mean_row_span(h->h_row_ptr.data(), col, h->m) * std::max(srow, WIN_LINE) < WIN_MIN_SPAN * WIN_L2_BYTES)
+            return 0;
+    }
+    const int64_t nseg = count_segments(pcs, col, W);
+    *nseg_out = nseg;
+    if (forced > 0) return W;
+    return (double)h->nnz >= WIN_MIN_SEG * (double)nseg ? W : 0;
 }
 
 }  // namespace
@@ -532,13 +716,43 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     pl.seq_max = std::max(1, std::min(pl.seq_max, CAP));
     pl.cap = std::max(pl.cap, std::min(CAP, pow2_ceil(pl.seq_max)));   // a row of T nonzeros fits one block
 
+    // column windows (chained mode): needs col_idx on the host and every row's columns sorted
     Inspection in;
-    inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in);
+    int64_t W = 0;
+    std::vector<int32_t> hcol;
+    {
+        const double srow = (double)pl.kw * (double)h->vsize;
+        const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
+        const int64_t forced = h->var.win_bytes != 0 ? h->var.win_bytes : env_bytes;
+        const bool maybe = h->nnz > 0 && forced >= 0 &&
+                           (forced > 0 || ((double)h->ncols * std::max(srow, WIN_LINE) > WIN_MIN_SPAN * WIN_L2_BYTES &&
+                                           srow >= WIN_MIN_ROW_BYTES));
+        if (maybe) {
+            hcol.resize((size_t)h->nnz);
+            HIPCHK(hipMemcpy(hcol.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
+            if (rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
+                std::vector<Piece> pcs;
+                Inspection tmp;
+                make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
+                W = window_cols(h, pl.kw, pcs, hcol.data(), h->var.win_bytes, &pl.nseg);
+            }
+        }
+    }
+    if (W > 0) {
+        inspect_windows(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, pl.cap, W, in);
+        pl.win_cols = W;
+        pl.nwin = (int)in.win_blk.size() - 1;
+        pl.nseg = (int64_t)in.vdest.size();
+    } else {
+        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in);
+        pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
+    }
     h->nv = (int64_t)in.vrow_ptr.size() - 1;
     h->nblk = (int)in.blk.size();
     h->nlong = (int)in.long_rows.size();
     h->nslots = in.nslots;
     h->plan = pl;
+    h->win_blk = in.win_blk;
 
     auto alloc_copy = [&](void **dst, const void *src, size_t bytes) -> hipError_t {
         hipError_t e = hipMalloc(dst, std::max<size_t>(bytes, 4));
@@ -558,6 +772,21 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     if (e == hipSuccess) e = hipMalloc(&h->d_xcol, h->b_bytes);
     if (e == hipSuccess) e = hipMalloc(&h->d_c, h->c_bytes);
     if (e == hipSuccess && h->nslots > 0) e = hipMalloc(&h->d_part, (size_t)h->nslots * k * h->vsize);
+    if (e == hipSuccess && W > 0) {
+        // window-major copies of col_idx / values (same padding as the originals)
+        const size_t nz = in.perm.size();
+        std::vector<char> hval((size_t)h->nnz * h->vsize), wval(nz * h->vsize + PAD_BYTES, 0);
+        std::vector<int32_t> wcol(nz + PAD_BYTES / 4, 0);
+        e = hipMemcpy(hval.data(), h->d_val, hval.size(), hipMemcpyDeviceToHost);
+        for (size_t q = 0; q < nz; ++q) {
+            const int64_t j = in.perm[q];
+            wcol[q] = hcol[(size_t)j];
+            std::memcpy(&wval[q * h->vsize], &hval[(size_t)j * h->vsize], h->vsize);
+        }
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_wcol, wcol.data(), wcol.size() * 4);
+        if (e == hipSuccess) e = alloc_copy(&h->d_wval, wval.data(), wval.size());
+        h->insp_bytes += wcol.size() * 4 + wval.size();
+    }
     if (e != hipSuccess) {
         free_plan(h);
         return fail(e == hipErrorOutOfMemory ? SPMM_HIP_ERR_NOMEM : SPMM_HIP_ERR_HIP,
@@ -659,7 +888,7 @@ int spmm_hip_stats_labels(char *buf, long buf_n) {
     if (!buf || buf_n <= 0) return fail(SPMM_HIP_ERR_ARG, "stats_labels: buffer");
     int n = snprintf(buf, (size_t)buf_n,
                      ",kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,split_rows,"
-                     "seq_max,panels,device");
+                     "seq_max,panels,windows,device");
     return (int)std::min<long>(n, buf_n - 1);
 }
 
@@ -671,8 +900,9 @@ int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n) {
     const int k = h->plan.k > 0 ? h->plan.k : 0;
     const double bytes = spmm_hip_bytes_alg(h->m, h->ncols, h->nnz, k, h->dtype);
     const double gbs = t[0] > 0 ? bytes / (t[0] * 1e-3) / 1e9 : 0.0;
-    int n = snprintf(buf, (size_t)buf_n, ",%.6f,%.6f,%.6f,%.6f,%.0f,%.2f,%.4f,%d,%d,%d,%d,%d", t[0], t[1], t[2], t[3],
-                     bytes, gbs, gbs / 8000.0, h->nblk, h->nlong, h->plan.seq_max, h->plan.npanels, h->device);
+    int n = snprintf(buf, (size_t)buf_n, ",%.6f,%.6f,%.6f,%.6f,%.0f,%.2f,%.4f,%d,%d,%d,%d,%d,%d", t[0], t[1], t[2], t[3],
+                     bytes, gbs, gbs / 8000.0, h->nblk, h->nlong, h->plan.seq_max, h->plan.npanels, h->plan.nwin,
+                     h->device);
     return (int)std::min<long>(n, buf_n - 1);
 }
 
@@ -691,6 +921,10 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
     out[9] = h->plan.cap;
     out[10] = h->plan.kw;
     out[11] = h->plan.npanels;
+    out[12] = h->plan.nwin;
+    out[13] = h->plan.win_cols;
+    out[14] = h->plan.nseg;
+    out[15] = 0;
     return SPMM_HIP_OK;
 }
 
@@ -715,10 +949,57 @@ int spmm_hip_destroy(spmm_hip_t *h) {
     return SPMM_HIP_OK;
 }
 
+int spmm_hip_debug_inspect(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
+                           int32_t cap, int64_t win_cols, spmm_hip_inspection_t *out) {
+    if (!row_ptr || !out || m < 0 || ncols < 0 || T < 1 || T > CAP || cap < T || cap > CAP || win_cols < 0)
+        return fail(SPMM_HIP_ERR_ARG, "debug_inspect: bad arguments");
+    std::memset(out, 0, sizeof(*out));
+    Inspection in;
+    if (win_cols > 0) {
+        if (!col_idx && row_ptr[m] > 0) return fail(SPMM_HIP_ERR_ARG, "debug_inspect: col_idx NULL");
+        if (!rows_sorted(row_ptr, col_idx, m)) return fail(SPMM_HIP_ERR_CSR, "debug_inspect: unsorted row");
+        inspect_windows(row_ptr, col_idx, m, ncols, T, cap, win_cols, in);
+    } else {
+        inspect(row_ptr, m, T, cap, in);
+        in.win_blk = {0, (int)in.blk.size()};
+    }
+    auto dup = [](const auto &v) {
+        using E = typename std::decay_t<decltype(v)>::value_type;
+        E *p = (E *)malloc(std::max<size_t>(v.size(), 1) * sizeof(E));
+        if (p && !v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(E));
+        return p;
+    };
+    out->nv = (int64_t)in.vrow_ptr.size() - 1;
+    out->nblk = (int64_t)in.blk.size();
+    out->nwin = (int64_t)in.win_blk.size() - 1;
+    out->nz = (int64_t)in.perm.size();
+    out->nlong = (int64_t)in.long_rows.size();
+    out->nslots = in.nslots;
+    out->vrow_ptr = dup(in.vrow_ptr);
+    out->vdest = dup(in.vdest);
+    out->blk = (int32_t *)dup(in.blk);
+    out->win_blk = dup(in.win_blk);
+    out->long_rows = (int32_t *)dup(in.long_rows);
+    out->perm = in.perm.empty() ? nullptr : dup(in.perm);
+    return SPMM_HIP_OK;
+}
+
+void spmm_hip_debug_free(spmm_hip_inspection_t *ins) {
+    if (!ins) return;
+    free(ins->vrow_ptr);
+    free(ins->vdest);
+    free(ins->blk);
+    free(ins->win_blk);
+    free(ins->long_rows);
+    free(ins->perm);
+    std::memset(ins, 0, sizeof(*ins));
+}
+
 #ifdef SPMM_TUNING
 // Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): kernel variant + inspector overrides; the
-// next run re-plans.  0 = policy default for seq_max / cap / panel_k.
-int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int seq_max, int cap, int panel_k) {
+// next run re-plans.  0 = policy default for seq_max / cap / panel_k / win_bytes (win_bytes < 0: no windows).
+int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int seq_max, int cap, int panel_k,
+                         int64_t win_bytes) {
     if (!h) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
     h->var.u = u;
     h->var.ntc = ntc;
@@ -727,6 +1008,7 @@ int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int se
     h->var.seq_max = seq_max;
     h->var.cap = cap;
     h->var.panel_k = panel_k;
+    h->var.win_bytes = win_bytes;
     const int k = h->plan.k;
     h->plan.k = -1;
     return k > 0 ? spmm_hip_plan(h, k) : SPMM_HIP_OK;

@@ -85,14 +85,11 @@ struct BGather {
     }
 };
 
-// Bijective XCD-aware remap (optional): hardware deals workgroups round-robin over the 8 XCDs, this gives each
-// XCD a contiguous run of blocks.  Speed only; any placement gives the same result.
 // One virtual row, nonzeros [a, e) of the LDS-staged block: U gathers in flight, then U FMAs in CSR order.
 template <typename T, int VEC, int U, typename Gather>
-__device__ __forceinline__ vec<T, VEC> row_dot(const int32_t *s_col, const T *s_val, int a, int e,
+__device__ __forceinline__ vec<T, VEC> row_dot(vec<T, VEC> acc, const int32_t *s_col, const T *s_val, int a, int e,
                                                const Gather &gather) {
     using V = vec<T, VEC>;
-    V acc = vzero<T, VEC>();
     int j = a;
     for (; j + U <= e; j += U) {
         V bv[U];
@@ -116,10 +113,16 @@ __device__ __forceinline__ vec<T, VEC> row_dot(const int32_t *s_col, const T *s_
 // ------------------------------------------------------------------------------------------------ row blocks
 // blk[b] = {first, end}: the virtual rows of block b (<= CAP nonzeros in all, <= CAP_ROWS rows); blocks holding
 // long serial rows come first in the table (they start at time 0), the rest in row order.  vrow_ptr indexes
-// the original col_idx / values.  SPLIT: vdest[v] >= 0 is v's C row, < 0 is partial slot -vdest[v]-1; otherwise
-// virtual row v IS C row v.  B and C point at the panel's first column; ld is their row stride (K); kw the panel
-// width.
-template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, bool SPLIT>
+// col_idx / values (the original arrays, or the window-major copy in chained mode).  B and C point at the panel's
+// first column; ld is their row stride (K); kw the panel width.  Destination of virtual row v by MODE:
+//   DEST_ROW   v IS C row v;
+//   DEST_SPLIT vdest[v] >= 0 is v's C row, < 0 is partial slot -vdest[v]-1;
+//   DEST_CHAIN vdest[v] = (d << 1) | cont with d as DEST_SPLIT; cont = 1: v continues the FMA chain of an earlier
+//              column window (one launch per window), so the accumulator starts from the value stored in the
+//              destination instead of 0 -- stored fp64/fp32 values are exact, so the chained result has the bits
+//              of one unbroken left-to-right chain.
+enum { DEST_ROW = 0, DEST_SPLIT = 1, DEST_CHAIN = 2 };
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE>
 __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
@@ -207,14 +210,20 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
         if (kk >= kw) continue;
         const BGather<T, VEC, BUF> gather(B, kk, ld, b_bytes);
         for (int r = grp; r < nrows; r += NG) {
-            const V acc = row_dot<T, VEC, U>(s_col, s_val, s_rp[r] - jb, s_rp[r + 1] - jb, gather);
             T *dst;
-            if constexpr (SPLIT) {
+            V acc = vzero<T, VEC>();
+            if constexpr (MODE == DEST_SPLIT) {
                 const int d = vdest[r0 + r];
                 dst = (d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld;
+            } else if constexpr (MODE == DEST_CHAIN) {
+                const int code = vdest[r0 + r];
+                const int d = code >> 1;
+                dst = (d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld;
+                if (code & 1) acc = *reinterpret_cast<const V *>(dst + kk);
             } else {
                 dst = C + (size_t)(r0 + r) * ld;
             }
+            acc = row_dot<T, VEC, U>(acc, s_col, s_val, s_rp[r] - jb, s_rp[r + 1] - jb, gather);
             vstore<T, VEC, NTC>(dst + kk, acc);
         }
     }

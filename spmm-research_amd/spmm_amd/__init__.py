@@ -24,6 +24,7 @@ LIB_DIR = PKG_ROOT / "lib"
 F64, F32 = 0, 1
 B_COL_MAJOR, B_ROW_MAJOR = 0, 1
 SEQ_MAX = 2048      # upper bound of the per-handle split length (MatrixFormat.seq_max)
+INFO_SLOTS = 16     # SPMM_HIP_INFO_SLOTS
 STATUS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP runtime error", -4: "no such HIP device",
           -5: "k mismatch", -6: "malformed CSR", -7: "size overflow"}
 
@@ -85,6 +86,13 @@ class _Features(C.Structure):
                 ("max_nnz_per_row", _i64)]
 
 
+class _Inspection(C.Structure):
+    _fields_ = [("nv", _i64), ("nblk", _i64), ("nwin", _i64), ("nz", _i64), ("nlong", _i64), ("nslots", _i64),
+                ("vrow_ptr", C.POINTER(C.c_int32)), ("vdest", C.POINTER(C.c_int32)), ("blk", C.POINTER(C.c_int32)),
+                ("win_blk", C.POINTER(C.c_int32)), ("long_rows", C.POINTER(C.c_int32)),
+                ("perm", C.POINTER(C.c_int64))]
+
+
 def _bind_hip(L: C.CDLL) -> C.CDLL:
     vp, i32, i64 = C.c_void_p, C.c_int32, _i64
     L.spmm_hip_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)]
@@ -100,6 +108,9 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_partition_rows.argtypes = [_i32p, i64, i64, i64, i64, C.POINTER(i64), C.POINTER(i64)]
     L.spmm_hip_bytes_alg.argtypes = [i64, i64, i64, i32, i32]
     L.spmm_hip_bytes_alg.restype = C.c_double
+    L.spmm_hip_debug_inspect.argtypes = [_i32p, _i32p, i64, i64, i32, i32, i64, C.POINTER(_Inspection)]
+    L.spmm_hip_debug_free.argtypes = [C.POINTER(_Inspection)]
+    L.spmm_hip_debug_free.restype = None
     L.spmm_hip_strerror.argtypes = [C.c_int]
     L.spmm_hip_strerror.restype = C.c_char_p
     L.spmm_hip_last_error_detail.restype = C.c_char_p
@@ -274,6 +285,26 @@ def bytes_alg(m: int, ncols: int, nnz: int, k: int, dtype: int = F64) -> float:
     return hip.spmm_hip_bytes_alg(m, ncols, nnz, k, dtype)
 
 
+def debug_inspect(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, T: int, cap: int,
+                  win_cols: int = 0) -> dict:
+    """The inspector's work decomposition (host only; spmm_hip_debug_inspect): virtual rows, destination codes,
+    workgroup blocks, per-window block ranges, the window-major nonzero permutation and the split rows."""
+    rp = np.ascontiguousarray(row_ptr, np.int32)
+    ci = np.ascontiguousarray(col_idx if len(col_idx) else np.zeros(1), np.int32)
+    ins = _Inspection()
+    _check("debug_inspect", hip.spmm_hip_debug_inspect(rp, ci, len(rp) - 1, ncols, T, cap, win_cols, C.byref(ins)))
+    try:
+        def arr(p, n):
+            return np.ctypeslib.as_array(p, (max(n, 1),))[:n].copy()
+        out = {"vrow_ptr": arr(ins.vrow_ptr, ins.nv + 1), "vdest": arr(ins.vdest, ins.nv if (win_cols or ins.nslots) else 0),
+               "blk": arr(ins.blk, 2 * ins.nblk).reshape(-1, 2), "win_blk": arr(ins.win_blk, ins.nwin + 1),
+               "long_rows": arr(ins.long_rows, 4 * ins.nlong).reshape(-1, 4), "nslots": int(ins.nslots),
+               "perm": arr(ins.perm, ins.nz) if ins.nz else None}
+    finally:
+        hip.spmm_hip_debug_free(C.byref(ins))
+    return out
+
+
 def device_count() -> int:
     n = C.c_int()
     hip.spmm_hip_device_count(C.byref(n))
@@ -332,7 +363,7 @@ class MatrixFormat:
         return {"kernel_ms": t[0], "transpose_ms": t[1], "h2d_ms": t[2], "d2h_ms": t[3]}
 
     def info(self) -> np.ndarray:
-        out = np.zeros(12, np.int64)
+        out = np.zeros(INFO_SLOTS, np.int64)
         _check("info", hip.spmm_hip_info(self._h, out))
         return out
 

@@ -146,7 +146,8 @@ def main():
                    "features": {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled", "skew",
                                                      "avg_num_neighbours", "cross_row_similarity")},
                    "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]),
-                   "split_rows": int(inf[6]), "blocks": int(inf[5]), **par}
+                   "split_rows": int(inf[6]), "blocks": int(inf[5]), "windows": int(inf[12]),
+                   "win_cols": int(inf[13]), "segments": int(inf[14]), **par}
             with open(out, "a") as f:
                 f.write(json.dumps(rec) + "\n")
             print(json.dumps({k2: rec[k2] for k2 in ("gen", "k", "ms", "gflops", "roofline_frac",
