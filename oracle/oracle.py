@@ -75,6 +75,8 @@ def ref_lib(vt: str = "d") -> C.CDLL:
                                     C.POINTER(C.c_long)]
         L.ref_metrics.argtypes = [_f64p, _f64p, C.c_long, _f64p]
         L.ref_set_threads.argtypes = [C.c_int]
+        L.ref_features.argtypes = [_i32p, _i32p, C.c_long, C.c_long, C.c_long, C.c_char_p, C.c_long]
+        L.ref_features.restype = C.c_long
         _ref[vt] = L
     return _ref[vt]
 
@@ -170,6 +172,30 @@ def ref_partition(row_ptr, nnz: int, workers: int, pos: int, vt: str = "d") -> t
     s, e = C.c_long(), C.c_long()
     ref_lib(vt).ref_partition(row_ptr, len(row_ptr) - 1, nnz, workers, pos, C.byref(s), C.byref(e))
     return s.value, e.value
+
+
+TWIN_FIELDS = ("nr_rows", "nr_cols", "avg_nnz_per_row", "std_nnz_per_row", "distribution", "placement", "bw",
+               "skew", "avg_num_neighbours", "cross_row_similarity", "seed")
+
+
+def ref_features(row_ptr, col_idx, ncols: int) -> dict:
+    """The reference feature extractor (csr_matrix_features_validation, csr_util_gen.c:889-990) on a CSR pattern:
+    the 11-field generator twin line it prints, parsed (plus the three 'extra features' of its first line)."""
+    rp = np.ascontiguousarray(row_ptr, np.int32)
+    ci = np.ascontiguousarray(col_idx if len(col_idx) else np.zeros(1), np.int32)
+    buf = C.create_string_buffer(1 << 16)
+    n = ref_lib("d").ref_features(rp, ci, len(rp) - 1, ncols, int(rp[-1]), buf, len(buf))
+    if n < 0:
+        raise RuntimeError("ref_features failed")
+    text = buf.value.decode()
+    twin = text[text.index("='") + 2:].split()
+    out = {}
+    for f, v in zip(TWIN_FIELDS, twin):
+        out[f] = v if f in ("distribution", "placement") else (int(v) if f in ("nr_rows", "nr_cols", "seed") else float(v))
+    extra = text[text.index("|") + 1:].split("|")[0].split()
+    out["num_neigh_std"], out["cross_row_neigh_avg"], out["cross_row_neigh_std"] = (float(x) for x in extra)
+    out["mem_footprint_mb"] = float(text.split("\n")[1].split()[0]) if "\n" in text else None
+    return out
 
 
 def ref_metrics(gold_d, test_d) -> np.ndarray:

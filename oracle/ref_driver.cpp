@@ -12,6 +12,9 @@
  *                    (spmv_bench.cpp:724-763 and :805-826)
  *   ref_partition    loop_partitioner_balance_prefix_sums (lib/parallel_util.h:141-165)
  *   ref_metrics      the 8 array_metrics calls of CheckAccuracy (spmv_bench.cpp:189-203)
+ *   ref_features     csr_matrix_features_validation (lib/storage_formats/csr_util/csr_util_gen.c:889-990, built as
+ *                    lib/aux/csr_util.c): the feature extractor that prints a matrix's 11-field generator "twin" line
+ *                    (rows cols avg std normal random bw skew neighbours cross_row_similarity 14) on stderr
  */
 #include <stdlib.h>
 #include <stdio.h>
@@ -30,9 +33,38 @@ extern "C" {
 #include "array_metrics.h"
 #include "storage_formats/matrix_market/matrix_market.h"
 #include "aux/csr_converter_double.h"
+#include "aux/csr_util.h"
 }
+#include <unistd.h>
 
 extern "C" {
+
+/* The reference extractor writes its result to stderr (and timings to stdout): capture both into a temporary file
+ * and return the stderr text (at most out_n - 1 chars).  Returns the length, or -1. */
+long ref_features(INT_T *row_ptr, INT_T *col_idx, long m, long n, long nnz, char *out, long out_n)
+{
+	fflush(stdout);
+	fflush(stderr);
+	FILE *tmp = tmpfile();
+	FILE *devnull = fopen("/dev/null", "w");
+	if (!tmp || !devnull) return -1;
+	int saved_err = dup(2), saved_out = dup(1);
+	dup2(fileno(tmp), 2);
+	dup2(fileno(devnull), 1);
+	csr_matrix_features_validation_csr_util((char *) "twin", row_ptr, col_idx, m, n, nnz);
+	fflush(stdout);
+	fflush(stderr);
+	dup2(saved_err, 2);
+	dup2(saved_out, 1);
+	close(saved_err);
+	close(saved_out);
+	fclose(devnull);
+	rewind(tmp);
+	long len = (long) fread(out, 1, out_n - 1, tmp);
+	out[len < 0 ? 0 : len] = 0;
+	fclose(tmp);
+	return len;
+}
 
 const char *ref_value_type(void) { return (sizeof(ValueType) == 8) ? "double" : "float"; }
 

@@ -7,13 +7,16 @@
 //     theta=std^2/avg) ("gamma", Marsaglia-Tsang), rounded, capped at nr_cols.
 //   * skew > 0: one row (seeded choice) gets degree avg*(1+skew) (capped at nr_cols); the other rows are scaled so
 //     that the total stays avg*nr_rows -- the feature skew = (max - avg)/avg then equals the parameter.
-//   * columns live in a window of width W_i = bw*nr_cols*(d+1)/(d-1) (the expected span of d uniform points in
-//     the window is then bw*nr_cols) centred on the diagonal; "random" placement = uniform positions inside it,
-//     "diagonal" = the same window with positions drawn from the central half (a tighter band).
 //   * neighbours: the row is laid out as R = d*(1 - nu/2) runs of consecutive columns separated by >= 1 free column;
 //     a run of length L contributes 2(L-1) to the row-neighbour count, so the mean over the row's nonzeros is nu.
-//   * cross-row similarity: row i copies whole runs of row i-1 until crs*d_{i-1} of row i-1's columns reappear
-//     (an exact copy is a neighbour at |dcol| = 0 <= 1); the rest of row i is new runs in its own window.
+//   * columns live in a window of width W_i = bw*nr_cols*(R_t+1)/(R_t-1) centred on the diagonal, R_t = the row's
+//     runs (copied + new, each placed independently): the expected span of R_t uniform points in the window is then
+//     bw*nr_cols.  A row keeps >= 2 runs when the requested span is wider than the row (else one run spans nothing).
+//     "random" placement = uniform positions inside the window, "diagonal" = positions from its central half.
+//   * cross-row similarity: row i copies runs of row i-1 until crs*d_{i-1} of row i-1's columns have a column
+//     within +-1 in row i (the feature's definition, csr_util_gen.c:553-610); a run is copied whole while that
+//     stays within the target, else its first L' columns (they match L'+1 of row i-1's columns).  New runs avoid
+//     +-1 contact with row i-1 where they can (a few random retries), so accidental matches do not inflate it.
 //   * values: seeded uniform [0.5, 1.5) (positive, cancellation-free, so 1e-10 checks are meaningful).
 // Determinism: every random stream is keyed by (seed, row, purpose); the copy chain restarts every SEG rows so
 // segments can be generated independently (any thread count, any row range) with identical output.
@@ -130,11 +133,11 @@ struct RowGen {
     std::vector<int32_t> prev, cur, tmp;
     std::vector<std::pair<int32_t, int32_t>> runs_prev, runs_cur;  // (start, length)
 
-    // window [lo, lo+W) for row i with degree d
-    void window(int64_t i, int64_t d, int64_t &lo, int64_t &W) const {
+    // window [lo, lo+W) for row i with degree d laid out as rt independently placed runs
+    void window(int64_t i, int64_t d, int64_t rt, int64_t &lo, int64_t &W) const {
         const int64_t n = p->nr_cols, m = p->nr_rows;
         double w = p->bw * (double)n;
-        if (d >= 2) w *= (double)(d + 1) / (double)(d - 1);
+        if (rt >= 2) w *= (double)(rt + 1) / (double)(rt - 1);
         W = std::max<int64_t>(std::llround(w), std::max<int64_t>(1, d));
         // room for the runs and their separating gaps
         W = std::min<int64_t>(n, std::max<int64_t>(W, 2 * d));
@@ -160,33 +163,61 @@ struct RowGen {
         Rng r((uint64_t)p->seed, (uint64_t)i, S_COLS);
         const double nu = std::min(2.0, p->avg_num_neighbours);
 
-        // 1. copy whole runs of the previous row
+        // 1. copy runs of the previous row: matched = row i-1 columns that get a column within +-1 in row i
+        int64_t copied_runs = 0;
         if (!runs_prev.empty() && p->cross_row_similarity > 0) {
-            int64_t target = std::llround(p->cross_row_similarity * (double)prev.size());
-            target = std::min<int64_t>(target, d);
+            const int64_t target = std::llround(p->cross_row_similarity * (double)prev.size());
             std::vector<int> order(runs_prev.size());
             for (size_t q = 0; q < order.size(); ++q) order[q] = (int)q;
             for (size_t q = order.size(); q > 1; --q) std::swap(order[q - 1], order[r.below((int64_t)q)]);
-            int64_t got = 0;
+            int64_t matched = 0;
             for (int q : order) {
-                if (got >= target) break;
-                auto run = runs_prev[q];
-                // whole runs keep the neighbour structure; only the row's own capacity truncates one
-                int32_t len = (int32_t)std::min<int64_t>(run.second, d - got);
-                runs_cur.push_back({run.first, len});
-                for (int32_t t = 0; t < len; ++t) cur.push_back(run.first + t);
-                got += len;
+                const int64_t need = target - matched, room = d - (int64_t)cur.size();
+                if (need <= 0 || room <= 0) break;
+                const auto run = runs_prev[q];
+                int64_t len = run.second;
+                if (len > need) len = std::max<int64_t>(1, need - 1);   // first len columns match len + 1
+                len = std::min(len, room);
+                for (int64_t t = 0; t < len; ++t) cur.push_back(run.first + (int32_t)t);
+                matched += (len < run.second) ? len + 1 : len;
+                ++copied_runs;
             }
         }
         std::sort(cur.begin(), cur.end());
 
-        // 2. new runs in the row's own window
+        // 2. the rest of the row.  The row should hold R_t runs: d*(1 - nu/2) for the neighbour count, and at least
+        // (1+bw)/(1-bw) when the requested span is wider than the row (R_t uniform runs span (R_t-1)/(R_t+1) of a
+        // window that cannot exceed n).  Copied runs count; if they already are R_t, the new columns grow them at
+        // their ends, otherwise R_t - copied new runs are placed in the row's own window.
         int64_t rest = d - (int64_t)cur.size();
+        int64_t Rt = std::max<int64_t>(1, std::llround((double)d * (1.0 - nu / 2.0)));
+        if (p->bw * (double)n >= 2.0 * (double)d) {
+            const double bwf = std::min(0.95, p->bw);
+            Rt = std::max<int64_t>(Rt, (int64_t)std::ceil((1.0 + bwf) / (1.0 - bwf) - 1e-9));
+        }
+        Rt = std::min<int64_t>(Rt, d);
+        if (rest > 0 && copied_runs >= Rt) {
+            std::vector<std::pair<int32_t, int32_t>> cr;   // copied runs as they stand in cur
+            for (size_t q = 0; q < cur.size();) {
+                size_t t = q + 1;
+                while (t < cur.size() && cur[t] == cur[t - 1] + 1) ++t;
+                cr.push_back({cur[q], (int32_t)(t - q)});
+                q = t;
+            }
+            for (int64_t tries = 0; rest > 0 && tries < 4 * d + 16; ++tries) {
+                auto &run = cr[r.below((int64_t)cr.size())];
+                const int64_t c = run.first + run.second;            // grow the run at its end
+                if (c < n && !taken(cur, c) && !taken(cur, c + 1)) {
+                    cur.insert(std::upper_bound(cur.begin(), cur.end(), (int32_t)c), (int32_t)c);
+                    ++run.second;
+                    --rest;
+                }
+            }
+        }
         if (rest > 0) {
+            const int64_t R = std::min<int64_t>(rest, std::max<int64_t>(1, Rt - copied_runs));
             int64_t lo, W;
-            window(i, d, lo, W);
-            int64_t R = std::max<int64_t>(1, std::llround((double)rest * (1.0 - nu / 2.0)));
-            R = std::min<int64_t>(R, rest);
+            window(i, d, R + copied_runs, lo, W);
             // run lengths: all 1, then the remaining units dealt at random
             std::vector<int64_t> L(R, 1);
             for (int64_t u = R; u < rest; ++u) L[r.below(R)]++;
@@ -201,10 +232,11 @@ struct RowGen {
             for (int64_t q = 0; q < R; ++q) {
                 int64_t start = (free_cells >= 0) ? lo + g[q] + off + q : lo + r.below(std::max<int64_t>(1, W - L[q]));
                 off += L[q];
-                // keep the run clear of copied columns (exact hits or adjacency); retry a few random starts
+                // keep the run clear of copied columns (exact hits or adjacency) and of +-1 contact with the
+                // previous row (accidental similarity); retry a few random starts
                 for (int tries = 0; tries < 8; ++tries) {
                     bool clash = false;
-                    for (int64_t t = -1; t <= L[q] && !clash; ++t) clash = taken(cur, start + t);
+                    for (int64_t t = -1; t <= L[q] && !clash; ++t) clash = taken(cur, start + t) || taken(prev, start + t);
                     if (!clash) break;
                     start = lo + r.below(std::max<int64_t>(1, W - L[q]));
                 }

@@ -13,6 +13,9 @@ What it writes (data only -- inputs and the reference's outputs; no reference so
                             plugin's C for fp64 and fp32 at K in {1,8,32,128}
   partition.npz             loop_partitioner_balance_prefix_sums boundaries for several row_ptr / worker counts
   metrics.npz               the 8 CheckAccuracy metrics (array_metrics) on (gold, test) pairs
+  features.npz              CSR patterns (the .mtx fixtures, hand-made edge cases, generator outputs) and what the
+                            reference's feature extractor (csr_matrix_features_validation, csr_util_gen.c:889-990)
+                            reports for them: avg, std, bw, skew, neighbours, cross-row similarity (the twin line)
 
 Every value in these files was computed by the reference's compiled code (oracle/_ref), except the inputs.
 """
@@ -235,6 +238,46 @@ def make_metrics():
     np.savez_compressed(OUT / "metrics.npz", **out)
 
 
+FEATURE_LINES = ["3000 3000 20 6.6667 normal random 0.3 100 0.95 0.5 14",
+                 "5000 4000 5 1.6667 normal random 0.05 0 0.05 0.05 14",
+                 "2000 2000 50 16.6667 normal random 0.6 1000 1.4 0.95 14",
+                 "1500 1500 100 33.3333 normal random 0.05 10000 1.9 0.5 14",
+                 "800 800 200 66.6667 gamma random 0.3 0 0.5 0.05 14",
+                 "4000 4000 10 3.3333 normal diagonal 0.3 0 0.95 0.95 14"]
+FEATURE_KEYS = ("avg_nnz_per_row", "std_nnz_per_row", "bw", "skew", "avg_num_neighbours", "cross_row_similarity")
+
+
+def make_features():
+    sys.path.insert(0, str(ROOT / "spmm-research_amd"))
+    import spmm_amd as S
+    out, names = {}, []
+    pats = {}
+    for f in sorted(MTX.glob("*.mtx")):
+        M, n, rp, ci, _ = O.ref_mtx_to_csr(str(f))
+        if M > 0 and len(ci) > 0:
+            pats[f.stem] = (rp, ci, n)
+    rng = np.random.default_rng(11)
+    for t in range(4):   # random sorted rows incl. empty ones and duplicates-free runs
+        m, n = 300 + 100 * t, 700
+        rows = [np.unique(rng.integers(0, n, rng.integers(0, 30))) if rng.random() > 0.2 else np.zeros(0, int)
+                for _ in range(m)]
+        rp = np.zeros(m + 1, np.int32)
+        rp[1:] = np.cumsum([len(r) for r in rows])
+        pats[f"random{t}"] = (rp, np.concatenate(rows).astype(np.int32), n)
+    for q, line in enumerate(FEATURE_LINES):
+        A = S.generate(S.gen_params(line))
+        pats[f"gen{q}"] = (A.row_ptr, A.col_idx, A.ncols)
+    for name, (rp, ci, n) in pats.items():
+        r = O.ref_features(rp, ci, n)
+        out[f"{name}.row_ptr"] = np.asarray(rp, np.int32)
+        out[f"{name}.col_idx"] = np.asarray(ci, np.int32)
+        out[f"{name}.ncols"] = np.int64(n)
+        out[f"{name}.features"] = np.array([r[k] for k in FEATURE_KEYS], np.float64)
+        names.append(name)
+    out["keys"] = np.array(FEATURE_KEYS)
+    np.savez_compressed(OUT / "features.npz", **out)
+
+
 def main():
     if not O.ref_available("d"):
         raise SystemExit("oracle/_ref not built: run `make -C oracle` in a container with /root/reference")
@@ -243,6 +286,7 @@ def main():
     make_spmm_cases()
     make_partition()
     make_metrics()
+    make_features()
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)
 
