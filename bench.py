@@ -49,6 +49,11 @@ def parse():
     return ap.parse_args()
 
 
+def engine_sha256() -> str:
+    import hashlib
+    return hashlib.sha256((ROOT / "spmm-research_amd" / "lib" / "libspmm_hip.so").read_bytes()).hexdigest()
+
+
 def cpu_baseline(A, k: int, budget_s: float) -> dict | None:
     """Reference compute_csr (oracle/_ref, compiled from /root/reference's sources) on this host, same matrix."""
     import numpy as np
@@ -176,10 +181,12 @@ def main():
     ncols_eff = p.nr_cols if N == 1 else int(np.unique(A.col_idx).size)
     bytes_launch = S.bytes_alg(A.m, ncols_eff, A.nnz, K, S.F64 if s == 8 else S.F32)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    # PMC traffic of THIS workload and THIS engine build (tools/collect_pmc.py, separate rocprofv3 --pmc passes)
     traffic = None
     try:
         pm = json.loads(Path(args.pmc_json).read_text())
-        if pm.get("workload") == args.gen and pm.get("k") == K and pm.get("dtype") == args.dtype and N == 1:
+        if (pm.get("workload") == args.gen and pm.get("k") == K and pm.get("dtype") == args.dtype and N == 1
+                and pm.get("nnz") == A.nnz and pm.get("engine_sha256") == engine_sha256()):
             traffic = pm.get("hbm_bytes_per_launch")
     except Exception:
         pass

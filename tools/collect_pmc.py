@@ -73,14 +73,18 @@ def main():
     for i, counters in enumerate(PASSES):
         res.update(run_pass(i, counters, outdir, bench_args, args.timeout))
     sys.path.insert(0, str(ROOT))
-    import bench  # for the workload defaults only
+    sys.path.insert(0, str(ROOT / "spmm-research_amd"))
+    import bench  # for the workload defaults and the engine fingerprint
     gen = args.gen or bench.GEN_LINE
     fetch_kib = res.get("FETCH_SIZE", {}).get("mean")
     write_kib = res.get("WRITE_SIZE", {}).get("mean")
     hbm = None
     if fetch_kib is not None and write_kib is not None:
         hbm = (2.0 * fetch_kib + write_kib) * 1024.0
-    summary = {"workload": gen, "k": args.k, "dtype": "f64", "kernel": KERNEL,
+    import spmm_amd as S
+    nnz = int(S.generate_row_ptr(S.gen_params(gen))[-1])
+    summary = {"workload": gen, "k": args.k, "dtype": "f64", "kernel": KERNEL, "nnz": nnz,
+               "engine_sha256": bench.engine_sha256(),
                "counters_per_launch": {k: v["mean"] for k, v in res.items()},
                "hbm_bytes_per_launch": hbm,
                "hbm_bytes_note": "(2*FETCH_SIZE + WRITE_SIZE) KiB -> bytes; L2 memory-side, includes Infinity-Cache hits",
