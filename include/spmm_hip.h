@@ -14,12 +14,13 @@
  *        The engine computes on a ROW-major device copy (B[col][K]); host column-major input is transposed on
  *        the device, outside the SpMM kernel.
  *   C    y = C ROW-major: y[i*K + n] (spmm_kernel_csr.cpp:93); every entry is written (0 for empty rows).
- * Numerics: each C entry of a row with at most T nonzeros is one left-to-right fused multiply-add chain from 0
- * over the row's nonzeros in CSR order -- the same bits as the reference kernel built with its own flags on an
- * FMA x86 host.  T (the split length, reported by spmm_hip_info out[8]) is chosen by the inspector per matrix and K
- * (64..2048) so no serial row outlasts the launch; SPMM_HIP_SEQ_MAX=<n> fixes it.  Longer rows are cut
- * into T-nonzero pieces whose partial sums are combined in piece order (deterministic run to run; within 1e-10
- * relative normwise for fp64).
+ * Numerics: every C entry is deterministic run to run and within 1e-10 relative normwise (fp64) of the exact sum
+ * (SURVEY §8a(ii)).  Rows flagged by spmm_hip_exact_rows -- normally all rows with at most T nonzeros -- are one
+ * left-to-right fused multiply-add chain from 0 over the row's nonzeros in CSR order: the same bits as the reference
+ * kernel built with its own flags on an FMA x86 host.  T (the split length, spmm_hip_info out[8]) is chosen by the
+ * inspector per matrix and K (64..2048) so no serial row outlasts the launch; SPMM_HIP_SEQ_MAX=<n> fixes it; longer
+ * rows are cut into T-nonzero pieces combined by a fixed tree.  For long rows at small K the inspector may also
+ * give one row several lane groups (vector lanes, out[16]); SPMM_HIP_LANES=-1 keeps every row <= T exact.
  */
 #ifndef SPMM_HIP_H
 #define SPMM_HIP_H
@@ -93,17 +94,27 @@ int spmm_hip_last_times(spmm_hip_t *h, double *out_ms);
 int spmm_hip_stats_labels(char *buf, long buf_n);
 int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
 
-#define SPMM_HIP_INFO_SLOTS 16
+#define SPMM_HIP_INFO_SLOTS 20
 
-/* Properties of the handle (out has SPMM_HIP_INFO_SLOTS = 16 slots): out[0]=m, out[1]=ncols, out[2]=nnz,
+/* Properties of the handle (out has SPMM_HIP_INFO_SLOTS = 20 slots): out[0]=m, out[1]=ncols, out[2]=nnz,
  * out[3]=k planned, out[4]=dtype, out[5]=workgroup blocks, out[6]=split rows, out[7]=device bytes held,
  * out[8]=split length T (rows with <= T nonzeros are bit-exact), out[9]=block capacity, out[10]=K-panel width,
  * out[11]=K panels, out[12]=column windows (1 = none; > 1: one launch per window, each row's FMA chain continued
  * through C from window to window, still bit-exact -- SPMM_HIP_WIN_BYTES=<bytes of B per window> forces them,
  * -1 disables), out[13]=window width in columns (0 = none), out[14]=virtual rows (row segments) over all windows,
- * out[15]=reserved (0). */
+ * out[15]=1 when workgroup blocks run in XCD-contiguous order (each XCD sweeps one eighth of the rows, so its L2
+ * holds only their B rows; SPMM_HIP_XCD=1 forces it, -1 disables it), out[16]=vector lanes: the most row groups one
+ * row may get (1 = one group per row; > 1 for long rows at small K, where a block holds fewer rows than groups: the
+ * row's nonzeros are dealt round-robin over L groups and the L partials added by a fixed tree -- deterministic,
+ * within the 1e-10 normwise contract, not the single chain; SPMM_HIP_LANES=<n> / -1 force / disable),
+ * out[17]=C rows computed as one left-to-right FMA chain (bit-identical to the reference; spmm_hip_exact_rows),
+ * out[18..19]=reserved (0). */
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
 
+/* Which C rows of the current plan are computed as ONE left-to-right FMA chain over the row in CSR order -- the
+ * reference kernel's exact operation sequence, so bit-identical to it (mask[i] = 1); the others (rows longer than
+ * the split length T, rows given vector lanes) are deterministic and within 1e-10 normwise.  mask has m bytes. */
+int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask);
 /* Device buffers owned by the handle (for callers that stage B/C themselves), row-major B of the planned k. */
 int spmm_hip_device_ptrs(spmm_hip_t *h, void **d_b_rowmajor, void **d_c);
 

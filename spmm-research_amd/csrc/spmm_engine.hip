@@ -67,6 +67,7 @@ constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may
 #define DEF_BUF 1
 #endif
 
+
 struct Plan {
     int k = -1;
     int kw = 0, npanels = 0;   // panel width (columns) and count
@@ -75,6 +76,9 @@ struct Plan {
     int64_t win_cols = 0;      // column-window width (0 = one window over all columns)
     int nwin = 1;              // column windows (one launch each per K panel)
     int64_t nseg = 0;          // virtual rows (segments) over all windows
+    int xcd = 0;               // 1 = XCD-contiguous block order (each XCD sweeps one eighth of the rows)
+    int lmax = 1;              // vector lanes: max groups per row (1 = every row one group, exact)
+    int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
 };
 
 struct Variant {
@@ -82,6 +86,8 @@ struct Variant {
     int seq_max = 0, cap = 0;  // 0 = inspector policy
     int panel_k = 0;           // 0 = inspector policy
     int64_t win_bytes = 0;     // 0 = inspector policy, < 0 = no column windows, > 0 = window of this many B bytes
+    int xcd = 0;               // 0 = inspector policy, < 0 = off, > 0 = XCD-contiguous block order
+    int lanes = 0;             // 0 = inspector policy, < 0 = off (exact rows), > 0 = vector lanes up to this many
 };
 
 }  // namespace
@@ -105,6 +111,8 @@ struct spmm_hip_handle {
     int2 *d_blk = nullptr;
     int4 *d_long_rows = nullptr;
     std::vector<int> win_blk;        // blocks of column window w: [win_blk[w], win_blk[w+1])
+    std::vector<int64_t> win_v;      // virtual rows of column window w: [win_v[w], win_v[w+1])
+    std::vector<uint8_t> exact;      // per C row: 1 = one left-to-right FMA chain (spmm_hip_exact_rows)
     int32_t *d_wcol = nullptr;       // chained mode: col_idx / values in window-major segment order
     void *d_wval = nullptr;
 
@@ -158,6 +166,7 @@ void free_plan(spmm_hip_t *h) {
     h->d_wcol = nullptr;
     h->d_wval = nullptr;
     h->win_blk.clear();
+    h->win_v.clear();
     h->d_vrow_ptr = h->d_vdest = nullptr;
     h->d_blk = nullptr;
     h->d_long_rows = nullptr;
@@ -173,22 +182,37 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * ld * sizeof(T), 0xFFFFFFFFull);
     if (h->plan.nwin > 1) {
         // chained mode: one launch per column window, in window order (each continues the chains of the last)
-        for (int w = 0; w < h->plan.nwin; ++w) {
-            const int b0 = h->win_blk[w], nb = h->win_blk[w + 1] - b0;
-            if (nb == 0) continue;
-            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, DEST_CHAIN><<<nb, WG, 0, s>>>(
-                h->d_vrow_ptr, h->d_wcol, (const T *)h->d_wval, h->d_blk + b0, nb, h->d_vdest, B, C, P, ld, kw, bb);
-        }
+        const int lmax = h->plan.lmax;
+        auto gow = [&](auto vl_c) {
+            for (int w = 0; w < h->plan.nwin; ++w) {
+                const int b0 = h->win_blk[w], nb = h->win_blk[w + 1] - b0;
+                if (nb == 0) continue;
+                spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, DEST_CHAIN, false, decltype(vl_c)::value>
+                    <<<nb, WG, 0, s>>>(h->d_vrow_ptr, h->d_wcol, (const T *)h->d_wval, h->d_blk + b0, nb, h->d_vdest,
+                                       B, C, P, ld, kw, bb, lmax);
+            }
+        };
+        if (lmax > 1) gow(std::true_type()); else gow(std::false_type());
         return;
     }
-    auto go = [&](auto mode_c) {
-        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value><<<h->nblk, WG, 0, s>>>(
-            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb);
+    auto go = [&](auto mode_c, auto xcd_c, auto vl_c) {
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
+                         decltype(vl_c)::value><<<h->nblk, WG, 0, s>>>(
+            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
+            h->plan.lmax);
     };
-    if (h->nslots > 0)
-        go(std::integral_constant<int, DEST_SPLIT>());
-    else
-        go(std::integral_constant<int, DEST_ROW>());
+    using split_c = std::integral_constant<int, DEST_SPLIT>;
+    using row_c = std::integral_constant<int, DEST_ROW>;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    const bool vl = h->plan.lmax > 1, sp = h->nslots > 0;
+    if (h->plan.xcd) {
+        if (sp) vl ? go(split_c(), T_(), T_()) : go(split_c(), T_(), F_());
+        else vl ? go(row_c(), T_(), T_()) : go(row_c(), T_(), F_());
+    } else {
+        if (sp) vl ? go(split_c(), F_(), T_()) : go(split_c(), F_(), F_());
+        else vl ? go(row_c(), F_(), T_()) : go(row_c(), F_(), F_());
+    }
 }
 
 // 32-bit buffer offsets for the B gather are valid while B fits 4 GiB.
@@ -206,8 +230,8 @@ bool try_variant(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStrea
 #define TV(U, NTC, DMA, BUF) try_variant<T, VEC, G, U, NTC, DMA, BUF>(h, B, C, P, ld, kw, s) ||
 template <typename T, int VEC, int G>
 bool launch_tuned(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
-    return TV(16, true, true, false) TV(16, true, false, false) TV(8, true, true, false) TV(8, true, false, false)
-        TV(24, true, true, false) TV(16, true, true, true) TV(16, true, false, true) TV(16, false, true, false) false;
+    return TV(16, true, true, false) TV(16, true, false, false) TV(16, true, true, true) TV(16, true, false, true)
+        false;
 }
 #endif
 
@@ -322,6 +346,7 @@ struct Inspection {
     std::vector<int2> blk;
     std::vector<int4> long_rows;
     std::vector<int> win_blk;       // chained mode: block offsets per window
+    std::vector<int64_t> win_v;     // chained mode: virtual-row offsets per window
     std::vector<int64_t> perm;      // chained mode: position in the window-major arrays -> original nonzero
     int heavy = 0;  // blocks moved to the front of the table
     int nslots = 0;
@@ -331,7 +356,8 @@ struct Inspection {
 // Longest-first for blocks whose longest row is a long serial chain (>= 256 nonzeros and >= 8x the mean row):
 // they are dispatched first and overlap the rest of the grid.  Everything else keeps row order, so all XCDs
 // sweep the same B window together.
-void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap, Inspection &out) {
+void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap, Inspection &out,
+                 bool heavy_first = true) {
     std::vector<int2> order;
     std::vector<int32_t> longest;
     int64_t start = v0;
@@ -349,7 +375,7 @@ void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap
         lmax = std::max<int32_t>(lmax, (int32_t)len);
     }
     const double mean = v1 > v0 ? (double)(vp[v1] - vp[v0]) / (double)(v1 - v0) : 0.0;
-    const int32_t heavy_len = (int32_t)std::max(256.0, 8.0 * mean);
+    const int32_t heavy_len = heavy_first ? (int32_t)std::max(256.0, 8.0 * mean) : INT32_MAX;
     std::vector<int> hv;
     for (size_t b = 0; b < order.size(); ++b)
         if (longest[b] >= heavy_len) hv.push_back((int)b);
@@ -361,7 +387,7 @@ void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap
 }
 
 // Virtual rows (rows longer than T cut into T-nonzero pieces) packed into blocks (one column window).
-void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
+void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool heavy_first = true) {
     out = Inspection();
     out.vrow_ptr.reserve((size_t)m + 1);
     out.vrow_ptr.push_back(rp[0]);
@@ -383,7 +409,7 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out) {
         }
     }
     if (!any_split) out.vdest.clear();
-    pack_blocks(out.vrow_ptr, 0, (int64_t)out.vrow_ptr.size() - 1, cap, out);
+    pack_blocks(out.vrow_ptr, 0, (int64_t)out.vrow_ptr.size() - 1, cap, out, heavy_first);
 }
 
 // Every row's columns non-decreasing (coo_to_csr's output).  Column windows keep each row's CSR order only then.
@@ -495,19 +521,22 @@ void inspect_windows(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
         pack_blocks(out.vrow_ptr, seg_off[w], seg_off[w + 1], cap, out);
         out.win_blk.push_back((int)out.blk.size());
     }
+    out.win_v = seg_off;
 }
 
 // Column-window policy (measured on MI355X; profiles/r01_windows_*.log).  A launch gathers one B row
 // (kw*s bytes, at least one 128-byte L2 line) per nonzero.  Processed in row order, consecutive rows sweep a band of
 // columns together, so the B lines in use at any moment are about one row span (max col - min col) wide: when the
-// span's lines fit an XCD's L2 (x = span lines / L2 < 1.5) the plain launch already gathers from L2 and windows only
+// span's lines fit an XCD's L2 (x = span lines / L2 < 1.5; < 3 for B rows of >= 256 bytes) the plain launch already
+// gathers from L2 and windows only
 // add launches and C round trips (72 K rows, 500 nnz, x = 1.4: 0.58 -> 0.60..0.66 ms; 100 nnz/row, bw 0.05:
 // 0.18 -> 0.30 ms).  When the span is wider, windows that keep an L2-sized slice of B hot pay, provided a row's
 // piece of one window stays long (>= 48 nonzeros): 500 nnz/row matrices 1.12-1.49x at K=32 and 1.54-1.96x at K=8;
 // config 2 (20 nnz over a 300 K-column span: 9 nnz per segment) and 100 nnz/row, bw 0.3 (7-27) lose 1.3-2.5x, as does
 // K=1 (its 8-byte gathers are request-bound).  Returns the window width in columns, 0 = no windows.
 constexpr double WIN_L2_BYTES = 4.0 * (1 << 20);   // L2 per XCD
-constexpr double WIN_MIN_SPAN = 1.5;               // row-span lines >= this many L2s
+constexpr double WIN_MIN_SPAN_NARROW = 1.5;        // row-span lines >= this many L2s, B rows <= 128 bytes
+constexpr double WIN_MIN_SPAN_WIDE = 3.0;          // ... B rows >= 256 bytes (K=128 unpanelled: x 1.6-1.8 lose, >= 3.4 win)
 constexpr double WIN_MIN_SEG = 48.0;               // mean nonzeros per segment at the chosen width
 constexpr double WIN_MIN_ROW_BYTES = 32.0;         // B row bytes: K=1..3 fp64 gathers are request-bound
 constexpr double WIN_LINE = 128.0;                 // L2 line
@@ -515,6 +544,32 @@ constexpr double WIN_LINE = 128.0;                 // L2 line
 // Window width in B bytes for a B row of srow bytes (measured best: 1-1.5 MB at K=8 fp64, 4-6 MB at K=32/128 fp64).
 double window_bytes(double srow) {
     return srow <= 64.0 ? 1.5 * (1 << 20) : srow <= 128.0 ? 3.0 * (1 << 20) : 6.0 * (1 << 20);
+}
+
+// Vector lanes (measured): worth it when a staged block fills <= 1/8 of its row groups with rows of
+// several gather batches -- 500 nnz/row: K=1 4.3-5x (2.20 -> 0.49 ms, 0.29 -> 0.059 ms), K=8 2x; 100 nnz/row K=1
+// 1.25x -- and not above (config 2 K=1, fill 0.4: 1.00x; 100 nnz/row K=8, fill 0.31: 0.93x; 500 nnz/row K=32, fill
+// 0.25: 0.65-0.99x), where it would only give up exact rows.
+constexpr double VL_ROW_FILL = 0.125;
+constexpr double VL_MIN_ROW = 32.0;   // mean virtual-row length (2 gather batches): tiny matrices stay exact
+
+// XCD-contiguous block order (policy).  The B rows an XCD's L2 must hold at a time are about one row span (the band
+// every row in flight sweeps) plus the rows in flight themselves: in the default round-robin order every XCD sees
+// the rows in flight of the whole chip (~1024 resident workgroups x rows per block), in XCD order only its own
+// eighth.  The order pays when that eighth brings the working set under an L2 while the chip-wide one is well
+// above it: rows of span << rows in flight (400 K rows, bw 0.01, K=32: 0.172 -> 0.154 ms); for spans wider than
+// the rows in flight it costs 6-12 % (config 2 K=1/8/32; bw 0.05-0.3 K=1), so it is not used there.
+constexpr double XCD_RESIDENT_BLOCKS = 1024.0;   // 256 CUs x 4 workgroups (VGPR-limited occupancy)
+bool xcd_order(const spmm_hip_t *h, double srow, double span, int cap) {
+    const int64_t env = env_int("SPMM_HIP_XCD", 0);
+    const int64_t forced = h->var.xcd != 0 ? h->var.xcd : env;
+    if (forced != 0) return forced > 0;
+    if (h->m < 8 * 64 || h->nnz == 0) return false;
+    const double avg = (double)h->nnz / (double)h->m;
+    const double rows_per_block = std::min((double)CAP_ROWS, std::max(1.0, (double)cap / std::max(avg, 1.0)));
+    const double in_flight = std::min((double)h->m, XCD_RESIDENT_BLOCKS * rows_per_block) * (double)h->ncols / (double)h->m;
+    const double line = std::max(srow, 8.0);
+    return (span + in_flight / 8.0) * line <= WIN_L2_BYTES && (span + in_flight) * line > 1.5 * WIN_L2_BYTES;
 }
 
 double mean_row_span(const int32_t *rp, const int32_t *col, int64_t m) {
@@ -540,7 +595,8 @@ int64_t window_cols(const spmm_hip_t *h, int kw, const std::vector<Piece> &pcs, 
     if (W >= h->ncols) return 0;
     if (forced == 0) {
         if (srow < WIN_MIN_ROW_BYTES) return 0;
-        if (mean_row_span(h->h_row_ptr.data(), col, h->m) * std::max(srow, WIN_LINE) < WIN_MIN_SPAN * WIN_L2_BYTES)
+        const double min_span = srow <= 128.0 ? WIN_MIN_SPAN_NARROW : WIN_MIN_SPAN_WIDE;
+        if (mean_row_span(h->h_row_ptr.data(), col, h->m) * std::max(srow, WIN_LINE) < min_span * WIN_L2_BYTES)
             return 0;
     }
     const int64_t nseg = count_segments(pcs, col, W);
@@ -716,7 +772,8 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     pl.seq_max = std::max(1, std::min(pl.seq_max, CAP));
     pl.cap = std::max(pl.cap, std::min(CAP, pow2_ceil(pl.seq_max)));   // a row of T nonzeros fits one block
 
-    // column windows (chained mode): needs col_idx on the host and every row's columns sorted
+    // XCD-contiguous order, else column windows (chained mode; needs every row's columns sorted); both decided from
+    // col_idx on the host
     Inspection in;
     int64_t W = 0;
     std::vector<int32_t> hcol;
@@ -724,35 +781,74 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         const double srow = (double)pl.kw * (double)h->vsize;
         const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
         const int64_t forced = h->var.win_bytes != 0 ? h->var.win_bytes : env_bytes;
-        const bool maybe = h->nnz > 0 && forced >= 0 &&
-                           (forced > 0 || ((double)h->ncols * std::max(srow, WIN_LINE) > WIN_MIN_SPAN * WIN_L2_BYTES &&
-                                           srow >= WIN_MIN_ROW_BYTES));
-        if (maybe) {
+        const bool b_big = (double)h->ncols * std::max(srow, WIN_LINE) > WIN_MIN_SPAN_NARROW * WIN_L2_BYTES;
+        const bool maybe_win = h->nnz > 0 && forced >= 0 && (forced > 0 || (b_big && srow >= WIN_MIN_ROW_BYTES));
+        const bool maybe_xcd = h->nnz > 0 && (double)h->ncols * srow > WIN_L2_BYTES;
+        if (maybe_win || maybe_xcd) {
             hcol.resize((size_t)h->nnz);
             HIPCHK(hipMemcpy(hcol.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
-            if (rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
-                std::vector<Piece> pcs;
-                Inspection tmp;
-                make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
-                W = window_cols(h, pl.kw, pcs, hcol.data(), h->var.win_bytes, &pl.nseg);
-            }
+        }
+        const double span = hcol.empty() ? (double)h->ncols : mean_row_span(h->h_row_ptr.data(), hcol.data(), h->m);
+        pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
+        if (maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
+            std::vector<Piece> pcs;
+            Inspection tmp;
+            make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
+            W = window_cols(h, pl.kw, pcs, hcol.data(), h->var.win_bytes, &pl.nseg);
         }
     }
     if (W > 0) {
+        pl.xcd = 0;
         inspect_windows(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, pl.cap, W, in);
         pl.win_cols = W;
         pl.nwin = (int)in.win_blk.size() - 1;
         pl.nseg = (int64_t)in.vdest.size();
     } else {
-        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in);
+        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd);
         pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
     }
     h->nv = (int64_t)in.vrow_ptr.size() - 1;
     h->nblk = (int)in.blk.size();
     h->nlong = (int)in.long_rows.size();
     h->nslots = in.nslots;
+    // vector lanes when the staged blocks hold fewer rows than row groups (long rows at small K), and
+    // the exact-row mask: rows <= T whose every virtual row sits in a block with L = 1
+    {
+        int vec, g;
+        lane_layout(pl.kw, k, h->vsize, vec, g);
+        const int ng = WG / g;
+        const int lcap = std::max(1, 64 / g);
+        const double nvr = (double)(in.vrow_ptr.size() - 1);
+        const double rows_per_block = in.blk.empty() ? 0.0 : nvr / (double)in.blk.size();
+        const double mean_vrow = nvr > 0 ? (double)h->nnz / nvr : 0.0;
+        const int env_l = env_int("SPMM_HIP_LANES", 0);
+        const int forced = h->var.lanes != 0 ? h->var.lanes : env_l;
+        if (forced != 0)
+            pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
+        else
+            pl.lmax = (h->nnz > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW) ? lcap : 1;
+        h->exact.assign((size_t)h->m, 1);
+        for (const int4 &lr : in.long_rows) h->exact[(size_t)lr.x] = 0;
+        if (pl.lmax > 1) {
+            for (const int2 &bk : in.blk) {
+                const int nrows = bk.y - bk.x;
+                if (nrows >= ng) continue;
+                int L = 1;
+                while (2 * L <= ng / nrows) L *= 2;
+                if (std::min(L, pl.lmax) <= 1) continue;
+                for (int v = bk.x; v < bk.y; ++v) {
+                    int64_t d = v;
+                    if (!in.vdest.empty()) d = (W > 0) ? (in.vdest[v] >> 1) : in.vdest[v];
+                    if (d >= 0) h->exact[(size_t)d] = 0;
+                }
+            }
+        }
+        pl.exact_rows = 0;
+        for (uint8_t e : h->exact) pl.exact_rows += e;
+    }
     h->plan = pl;
     h->win_blk = in.win_blk;
+    h->win_v = in.win_v;
 
     auto alloc_copy = [&](void **dst, const void *src, size_t bytes) -> hipError_t {
         hipError_t e = hipMalloc(dst, std::max<size_t>(bytes, 4));
@@ -924,7 +1020,16 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
     out[12] = h->plan.nwin;
     out[13] = h->plan.win_cols;
     out[14] = h->plan.nseg;
-    out[15] = 0;
+    out[15] = h->plan.xcd;
+    out[16] = h->plan.lmax;
+    out[17] = h->plan.exact_rows;
+    out[18] = out[19] = 0;
+    return SPMM_HIP_OK;
+}
+
+int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask) {
+    if (!h || !mask || h->plan.k < 1) return fail(SPMM_HIP_ERR_ARG, "exact_rows: handle not planned");
+    if (h->m > 0) std::memcpy(mask, h->exact.data(), (size_t)h->m);
     return SPMM_HIP_OK;
 }
 
@@ -999,7 +1104,7 @@ void spmm_hip_debug_free(spmm_hip_inspection_t *ins) {
 // Tuning build only (lib/libspmm_hip_tune.so, tools/tune_kernel.py): kernel variant + inspector overrides; the
 // next run re-plans.  0 = policy default for seq_max / cap / panel_k / win_bytes (win_bytes < 0: no windows).
 int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int seq_max, int cap, int panel_k,
-                         int64_t win_bytes) {
+                         int64_t win_bytes, int xcd, int lanes) {
     if (!h) return fail(SPMM_HIP_ERR_ARG, "tune_select: bad handle");
     h->var.u = u;
     h->var.ntc = ntc;
@@ -1009,6 +1114,8 @@ int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int se
     h->var.cap = cap;
     h->var.panel_k = panel_k;
     h->var.win_bytes = win_bytes;
+    h->var.xcd = xcd;
+    h->var.lanes = lanes;
     const int k = h->plan.k;
     h->plan.k = -1;
     return k > 0 ? spmm_hip_plan(h, k) : SPMM_HIP_OK;

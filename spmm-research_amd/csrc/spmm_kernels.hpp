@@ -110,6 +110,29 @@ __device__ __forceinline__ vec<T, VEC> row_dot(vec<T, VEC> acc, const int32_t *s
     return acc;
 }
 
+// Strided piece of a virtual row for vector lanes: nonzeros a, a+L, a+2L, ... < e (L = 1: the whole row, in order).
+template <typename T, int VEC, int U, typename Gather>
+__device__ __forceinline__ vec<T, VEC> row_dot_strided(vec<T, VEC> acc, const int32_t *s_col, const T *s_val, int a,
+                                                       int e, int L, const Gather &gather) {
+    using V = vec<T, VEC>;
+    for (int j = a; j < e; j += U * L) {
+        V bv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u * L < e) bv[u] = gather(s_col[j + u * L]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u * L < e) vfma(acc, s_val[j + u * L], bv[u]);
+    }
+    return acc;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void vshfl_add(vec<T, N> &acc, int off) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc.v[i] += __shfl_xor(acc.v[i], off);
+}
+
 // ------------------------------------------------------------------------------------------------ row blocks
 // blk[b] = {first, end}: the virtual rows of block b (<= CAP nonzeros in all, <= CAP_ROWS rows); blocks holding
 // long serial rows come first in the table (they start at time 0), the rest in row order.  vrow_ptr indexes
@@ -121,15 +144,29 @@ __device__ __forceinline__ vec<T, VEC> row_dot(vec<T, VEC> acc, const int32_t *s
 //              column window (one launch per window), so the accumulator starts from the value stored in the
 //              destination instead of 0 -- stored fp64/fp32 values are exact, so the chained result has the bits
 //              of one unbroken left-to-right chain.
+// XCD: workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8 share one); the bijective remap gives each
+// XCD one contiguous eighth of the block table, i.e. of the rows, so an XCD's L2 only ever holds the B rows of its
+// own row range (speed only: any placement computes the same result).
 enum { DEST_ROW = 0, DEST_SPLIT = 1, DEST_CHAIN = 2 };
-template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE>
+__device__ __forceinline__ int xcd_block(int w, int nb) {
+    const int x = w & 7, i = w >> 3, q = nb >> 3, r = nb & 7;
+    return x * q + (x < r ? x : r) + i;
+}
+// VL (vector lanes, SURVEY §8f "K=1 SpMV specialisation"): when a block holds fewer rows than row groups (long
+// rows at small K: K=1 has 256 one-lane groups but a 2048-nonzero block holds 4 rows of 500), each row is given
+// L = min(lmax, pow2floor(NG / rows)) groups; sub-lane l sums nonzeros l, l+L, ... and the L partials are added by a
+// fixed xor-shuffle tree.  Deterministic, within the 1e-10 normwise contract, but not the reference's single chain:
+// rows of blocks with L > 1 are reported as inexact (spmm_hip_exact_rows).  L is block-uniform; L = 1 blocks are
+// exactly the plain kernel.
+template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE, bool XCD = false,
+          bool VL = false>
 __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
                                                        const int2 *__restrict__ blk, int nblk,
                                                        const int32_t *__restrict__ vdest,
                                                        const T *__restrict__ B, T *__restrict__ C, T *__restrict__ P,
-                                                       int ld, int kw, uint32_t b_bytes) {
+                                                       int ld, int kw, uint32_t b_bytes, int lmax) {
     constexpr int SVN = 16 / (int)sizeof(T);
     constexpr int CAPP = CAP + 4;                         // staged window starts at a 16-byte boundary
     __shared__ __attribute__((aligned(16))) int32_t s_rp[CAP_ROWS + 64];
@@ -138,7 +175,7 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     using V = vec<T, VEC>;
     constexpr int NG = WG / G;
 
-    const int b = (int)blockIdx.x;
+    const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int tid = threadIdx.x;
     const int2 rr = blk[b];
     const int r0 = rr.x, r1 = rr.y;
@@ -204,12 +241,21 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     __syncthreads();
 
     const int lane = tid % G;
-    const int grp = tid / G;
+    int L = 1;
+    if constexpr (VL) {
+        if (nrows < NG) {
+            L = 1 << (31 - __builtin_clz(NG / nrows));
+            L = L < lmax ? L : lmax;
+        }
+    }
+    const int sub = (tid / G) % L;               // 0 when L = 1
+    const int grp = tid / (G * L);
+    const int rstep = NG / L;
     for (int kc = 0; kc < kw; kc += G * VEC) {
         const int kk = kc + lane * VEC;
         if (kk >= kw) continue;
         const BGather<T, VEC, BUF> gather(B, kk, ld, b_bytes);
-        for (int r = grp; r < nrows; r += NG) {
+        for (int r = grp; r < nrows; r += rstep) {
             T *dst;
             V acc = vzero<T, VEC>();
             if constexpr (MODE == DEST_SPLIT) {
@@ -219,12 +265,18 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
                 const int code = vdest[r0 + r];
                 const int d = code >> 1;
                 dst = (d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld;
-                if (code & 1) acc = *reinterpret_cast<const V *>(dst + kk);
+                if ((code & 1) && sub == 0) acc = *reinterpret_cast<const V *>(dst + kk);
             } else {
                 dst = C + (size_t)(r0 + r) * ld;
             }
-            acc = row_dot<T, VEC, U>(acc, s_col, s_val, s_rp[r] - jb, s_rp[r + 1] - jb, gather);
-            vstore<T, VEC, NTC>(dst + kk, acc);
+            if constexpr (VL) {
+                acc = row_dot_strided<T, VEC, U>(acc, s_col, s_val, s_rp[r] - jb + sub, s_rp[r + 1] - jb, L, gather);
+                for (int off = (G * L) >> 1; off >= G; off >>= 1) vshfl_add(acc, off);   // fixed tree over sub-lanes
+                if (sub == 0) vstore<T, VEC, NTC>(dst + kk, acc);
+            } else {
+                acc = row_dot<T, VEC, U>(acc, s_col, s_val, s_rp[r] - jb, s_rp[r + 1] - jb, gather);
+                vstore<T, VEC, NTC>(dst + kk, acc);
+            }
         }
     }
 }

@@ -24,7 +24,7 @@ LIB_DIR = PKG_ROOT / "lib"
 F64, F32 = 0, 1
 B_COL_MAJOR, B_ROW_MAJOR = 0, 1
 SEQ_MAX = 2048      # upper bound of the per-handle split length (MatrixFormat.seq_max)
-INFO_SLOTS = 16     # SPMM_HIP_INFO_SLOTS
+INFO_SLOTS = 20     # SPMM_HIP_INFO_SLOTS
 STATUS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP runtime error", -4: "no such HIP device",
           -5: "k mismatch", -6: "malformed CSR", -7: "size overflow"}
 
@@ -104,6 +104,7 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_stats.argtypes = [vp, C.c_char_p, C.c_long]
     L.spmm_hip_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
     L.spmm_hip_device_ptrs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+    L.spmm_hip_exact_rows.argtypes = [vp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")]
     L.spmm_hip_destroy.argtypes = [vp]
     L.spmm_hip_partition_rows.argtypes = [_i32p, i64, i64, i64, i64, C.POINTER(i64), C.POINTER(i64)]
     L.spmm_hip_bytes_alg.argtypes = [i64, i64, i64, i32, i32]
@@ -366,6 +367,12 @@ class MatrixFormat:
         out = np.zeros(INFO_SLOTS, np.int64)
         _check("info", hip.spmm_hip_info(self._h, out))
         return out
+
+    def exact_rows(self) -> np.ndarray:
+        """bool[m]: rows computed as the reference's single left-to-right FMA chain (bit-identical to it)."""
+        mask = np.zeros(max(self.m, 1), np.uint8)
+        _check("exact_rows", hip.spmm_hip_exact_rows(self._h, mask))
+        return mask[:self.m].astype(bool)
 
     @property
     def seq_max(self) -> int:

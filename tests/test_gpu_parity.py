@@ -1,9 +1,9 @@
 """GPU parity: the HIP engine (through its C ABI) against the oracle and the reference's golden vectors.
 
-Bar: indexing bit-exact; for rows of <= T nonzeros (T = the handle's split length, 16..2048,
-chosen by the inspector) the engine computes each C entry as one left-to-right FMA chain, so it must equal the
-reference kernel BIT FOR BIT (fp64 and fp32); longer rows are split with a fixed-order combine and must satisfy
-the normwise criterion |C - gold| <= TOL * max(|gold|, sum_j |a_ij b_jn|), TOL = 1e-10 (fp64) / n * 2^-23
+Bar: indexing bit-exact; every row the engine reports exact (spmm_hip_exact_rows: rows of <= T
+nonzeros, T = the handle's split length, 64..2048, that were not given vector lanes) is one left-to-right FMA chain,
+so it must equal the reference kernel BIT FOR BIT (fp64 and fp32); the other rows (split rows, vector lanes) must
+be deterministic and satisfy the normwise criterion |C - gold| <= TOL * max(|gold|, sum_j |a_ij b_jn|), TOL = 1e-10 (fp64) / n * 2^-23
 (fp32, n = row length), and be identical run to run.  At full size (config 2: 1M x 1M, 20M nnz) parity is checked on a row sample plus size-independent
 properties (determinism, linearity in B, layout equivalence).
 """
@@ -31,20 +31,20 @@ def env():
     return torch, S, O
 
 
-def gpu_spmm(S, A_rp, A_ci, vals, m, n, x_colmajor, k, want_seq_max=False):
+def gpu_spmm(S, A_rp, A_ci, vals, m, n, x_colmajor, k, want_exact=False):
     mf = S.csr_to_format(A_rp, A_ci, vals, m, n, len(A_ci), k, 0)
     y = np.full(m * k, np.nan, vals.dtype)          # garbage in: every entry must be written
     mf.spmm(np.ascontiguousarray(x_colmajor, vals.dtype), y, k)
-    T = mf.seq_max
+    ex = mf.exact_rows()
+    assert ex[np.diff(A_rp) > mf.seq_max].sum() == 0     # split rows are never reported exact
     mf.close()
-    return (y.reshape(m, k), T) if want_seq_max else y.reshape(m, k)
+    return (y.reshape(m, k), ex) if want_exact else y.reshape(m, k)
 
 
-def check_split_aware(O, A_rp, A_ci, vals, ncols, x, k, y, T, tol):
-    """Rows <= T bit-exact vs the oracle; split rows normwise vs the Kahan gold."""
+def check_split_aware(O, A_rp, A_ci, vals, ncols, x, k, y, exact, tol):
+    """Exact rows bit-exact vs the oracle; the rest normwise vs the Kahan gold."""
     seq = O.spmm(A_rp, A_ci, vals, ncols, x, k)
-    deg = np.diff(A_rp)
-    short = deg <= T
+    short = exact
     assert bits_equal(y[short], seq[short])
     if (~short).any():
         g, absdot = O.gold(A_rp, A_ci, vals.astype(np.float64), ncols, x.astype(np.float64), k)
@@ -72,12 +72,10 @@ def test_golden_spmm_cases_bitwise(env, golden):
             if f"{c}.x.k{k}" not in d.files:
                 continue
             x = d[f"{c}.x.k{k}"]
-            y, T = gpu_spmm(S, rp, ci, va, m, ncols, x, k, want_seq_max=True)
-            short = np.diff(rp) <= T
+            y, short = gpu_spmm(S, rp, ci, va, m, ncols, x, k, want_exact=True)
             assert bits_equal(y[short], d[f"{c}.y_d.k{k}"][short]), (c, k)
-            check_split_aware(O, rp, ci, va, ncols, x, k, y, T, TOL_F64)
-            yf, T = gpu_spmm(S, rp, ci, va.astype(np.float32), m, ncols, x.astype(np.float32), k, want_seq_max=True)
-            short = np.diff(rp) <= T
+            check_split_aware(O, rp, ci, va, ncols, x, k, y, short, TOL_F64)
+            yf, short = gpu_spmm(S, rp, ci, va.astype(np.float32), m, ncols, x.astype(np.float32), k, want_exact=True)
             assert bits_equal(yf[short], d[f"{c}.y_f.k{k}"][short]), (c, k, "f32")
             n += 1
     assert n >= 15
@@ -104,12 +102,11 @@ def test_generated_bitwise_all_k(env, k):
     torch, S, O = env
     A = S.generate(S.gen_params("30000 24000 20 6.6667 normal random 0.3 50 0.95 0.5 14"))
     x = O.drand48(7 + k, A.ncols * k)
-    y, T = gpu_spmm(S, A.row_ptr, A.col_idx, A.values, A.m, A.ncols, x, k, want_seq_max=True)
-    check_split_aware(O, A.row_ptr, A.col_idx, A.values, A.ncols, x, k, y, T, TOL_F64)
+    y, ex = gpu_spmm(S, A.row_ptr, A.col_idx, A.values, A.m, A.ncols, x, k, want_exact=True)
+    check_split_aware(O, A.row_ptr, A.col_idx, A.values, A.ncols, x, k, y, ex, TOL_F64)
     vf, xf = A.values.astype(np.float32), x.astype(np.float32)
-    yf, T = gpu_spmm(S, A.row_ptr, A.col_idx, vf, A.m, A.ncols, xf, k, want_seq_max=True)
+    yf, short = gpu_spmm(S, A.row_ptr, A.col_idx, vf, A.m, A.ncols, xf, k, want_exact=True)
     seqf = O.spmm(A.row_ptr, A.col_idx, vf, A.ncols, xf, k)
-    short = np.diff(A.row_ptr) <= T
     assert bits_equal(yf[short], seqf[short])
 
 
@@ -122,12 +119,12 @@ def test_long_rows_split_path(env, dtype):
     x = O.drand48(5, A.ncols * k)
     vals = A.values if dtype == "f64" else A.values.astype(np.float32)
     xx = x if dtype == "f64" else x.astype(np.float32)
-    y1, T = gpu_spmm(S, A.row_ptr, A.col_idx, vals, A.m, A.ncols, xx, k, want_seq_max=True)
+    y1, ex = gpu_spmm(S, A.row_ptr, A.col_idx, vals, A.m, A.ncols, xx, k, want_exact=True)
     y2 = gpu_spmm(S, A.row_ptr, A.col_idx, vals, A.m, A.ncols, xx, k)
     assert bits_equal(y1, y2), "long-row combine must be deterministic"
     seq = O.spmm(A.row_ptr, A.col_idx, vals, A.ncols, xx, k)
     deg = np.diff(A.row_ptr)
-    long_rows = deg > T
+    long_rows = ~ex
     assert long_rows.sum() >= 1
     assert bits_equal(y1[~long_rows], seq[~long_rows])
     # gold of the inputs the kernel actually saw (fp32-rounded for f32), so only summation error remains
@@ -197,24 +194,24 @@ def test_row_shards_equal_whole(env, monkeypatch):
     x = O.drand48(1, A.ncols * k)
 
     def run_all():
-        whole, tw = gpu_spmm(S, A.row_ptr, A.col_idx, A.values, A.m, A.ncols, x, k, want_seq_max=True)
+        whole, tw = gpu_spmm(S, A.row_ptr, A.col_idx, A.values, A.m, A.ncols, x, k, want_exact=True)
         parts, ts = [], []
         for w in range(3):
             r0, r1 = S.partition_rows(A.row_ptr, A.nnz, 3, w)
             sh = S.generate_rows(p, r0, r1)
-            y, t = gpu_spmm(S, sh.row_ptr, sh.col_idx, sh.values, sh.m, A.ncols, x, k, want_seq_max=True)
+            y, t = gpu_spmm(S, sh.row_ptr, sh.col_idx, sh.values, sh.m, A.ncols, x, k, want_exact=True)
             parts.append(y)
             ts.append(t)
-        return whole, np.concatenate(parts), min([tw] + ts)
+        return whole, np.concatenate(parts), tw & np.concatenate(ts)
 
-    whole, parts, tmin = run_all()
-    short = np.diff(A.row_ptr) <= tmin
+    whole, parts, short = run_all()
     assert bits_equal(parts[short], whole[short])
     g, absdot = O.gold(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
     assert O.normwise_ok(parts, g, absdot, TOL_F64).all()
     monkeypatch.setenv("SPMM_HIP_SEQ_MAX", "2048")
-    whole, parts, tmin = run_all()
-    assert tmin == 2048
+    monkeypatch.setenv("SPMM_HIP_LANES", "-1")
+    whole, parts, short = run_all()
+    assert short.all()
     assert bits_equal(parts, whole)
 
 
@@ -252,7 +249,7 @@ def test_full_size_config2_properties(env):
     x_col = np.ascontiguousarray(B1.cpu().numpy().T).ravel()
     want = O.spmm(sub_rp, sub_ci, sub_va, A.ncols, x_col, k)
     got = C1.cpu().numpy()[rows]
-    short = np.diff(sub_rp) <= mf.seq_max
+    short = mf.exact_rows()[rows]
     assert bits_equal(got[short], want[short])
     g, absdot = O.gold(sub_rp, sub_ci, sub_va, A.ncols, x_col, k)
     assert O.normwise_ok(got, g, absdot, TOL_F64).all()

@@ -17,6 +17,8 @@ for f in sys.argv[1:]:
     for r in rows:
         v, p = r["variant"], r["plan"]
         segs = max(p.get("segments", 1), 1)
-        print(f"  win={v.get('WIN_BYTES', 0):>9} T={v['SEQ_MAX']:>4} {r['median_ms']:8.4f} ms  x{base / r['median_ms']:5.2f}"
+        print(f"  U={v['U']:>2} win={v.get('WIN_BYTES', 0):>9} xcd={v.get('XCD', 0):>2} lanes={v.get('LANES', 0):>2}"
+              f" -> L{p.get('lmax', '-')}/x{p.get('xcd', '-')} exact={p.get('exact_rows', '-')} T={v['SEQ_MAX']:>4}"
+              f" {r['median_ms']:8.4f} ms  x{base / r['median_ms']:5.2f}"
               f"  windows={p.get('windows', 1):>4} segs={segs:>9} nnz/seg={(head['nnz'] if head else 0) / segs:7.1f}"
               f"  close={r['close']}")

@@ -39,7 +39,7 @@ def dataset_lines(args) -> list[str]:
     return lines[args.offset::args.stride]
 
 
-def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, seq_max):
+def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, exact):
     """Oracle on a row sample: sub-CSR of the sampled rows with its columns renumbered, B rows fetched from HBM."""
     import torch
     m = A.m
@@ -55,7 +55,7 @@ def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, seq_max):
     vv = vals.astype(dtype)
     want = O.spmm(sub_rp, inv.astype(np.int32), vv, len(ucols), x_col.astype(dtype), k)
     got = C_dev.index_select(0, torch.from_numpy(rows.astype(np.int64)).to(C_dev.device)).cpu().numpy()
-    seq = deg[rows] <= seq_max
+    seq = exact[rows]
     it = np.int64 if dtype == np.float64 else np.int32
     bit_ok = bool(np.array_equal(got[seq].view(it), want[seq].view(it)))
     g, absdot = O.gold(sub_rp, inv.astype(np.int32), vv.astype(np.float64), len(ucols), x_col.astype(np.float64), k)
@@ -138,7 +138,7 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.iters
             bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
-            par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.seq_max)
+            par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows())
             inf = mf.info()
             rec = {"gen": line, "k": k, "dtype": args.dtype, "m": int(A.m), "nnz": int(A.nnz), "ms": ms,
                    "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9, "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9,
@@ -147,7 +147,8 @@ def main():
                                                      "avg_num_neighbours", "cross_row_similarity")},
                    "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]),
                    "split_rows": int(inf[6]), "blocks": int(inf[5]), "windows": int(inf[12]),
-                   "win_cols": int(inf[13]), "segments": int(inf[14]), **par}
+                   "win_cols": int(inf[13]), "segments": int(inf[14]), "xcd": int(inf[15]), "lmax": int(inf[16]),
+                   "exact_rows": int(inf[17]), **par}
             with open(out, "a") as f:
                 f.write(json.dumps(rec) + "\n")
             print(json.dumps({k2: rec[k2] for k2 in ("gen", "k", "ms", "gflops", "roofline_frac",

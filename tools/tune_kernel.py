@@ -18,12 +18,13 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 
-# (U, NTC, DMA, BUF, seq_max, cap, panel_k[, win_bytes]): 0 = inspector policy default (win_bytes -1 = no windows)
+# (U, NTC, DMA, BUF, seq_max, cap, panel_k[, win_bytes[, xcd]]): 0 = inspector policy default (win_bytes -1 = no
+# windows; xcd 1 = XCD-contiguous block order, -1 = off)
 VARIANTS = [(16, 1, 0, 1, 0, 0, 0), (16, 1, 1, 1, 0, 0, 0), (16, 1, 0, 0, 0, 0, 0), (8, 1, 0, 1, 0, 0, 0),
             (16, 1, 0, 1, 2048, 0, 0), (16, 1, 0, 1, 64, 0, 0), (16, 1, 0, 1, 128, 0, 0), (16, 1, 0, 1, 256, 0, 0),
             (16, 1, 0, 1, 512, 0, 0), (16, 1, 0, 1, 0, 1024, 0), (16, 1, 0, 1, 0, 2048, 0), (16, 1, 0, 1, 0, 4096, 0),
             (16, 1, 0, 1, 0, 0, 16), (16, 1, 0, 1, 0, 0, 64), (16, 1, 0, 1, 0, 0, 4096)]
-FIELDS = ("U", "NTC", "DMA", "BUF", "SEQ_MAX", "CAP", "PANEL_K", "WIN_BYTES")
+FIELDS = ("U", "NTC", "DMA", "BUF", "SEQ_MAX", "CAP", "PANEL_K", "WIN_BYTES", "XCD", "LANES")
 
 
 def main():
@@ -40,7 +41,7 @@ def main():
     import torch
     import spmm_amd as S
     T = S._bind_hip(C.CDLL(str(ROOT / "spmm-research_amd" / "lib" / "libspmm_hip_tune.so")))
-    T.spmm_hip_tune_select.argtypes = [C.c_void_p] + [C.c_int] * 7 + [C.c_int64]
+    T.spmm_hip_tune_select.argtypes = [C.c_void_p] + [C.c_int] * 7 + [C.c_int64, C.c_int, C.c_int]
 
     A = S.generate(S.gen_params(args.gen))
     k = args.k
@@ -61,7 +62,7 @@ def main():
     variants = VARIANTS if not args.only else [VARIANTS[int(i)] for i in args.only.split(",")]
     if args.variants:
         variants = [tuple(int(x) for x in v.split(",")) for v in args.variants.split(";")]
-    variants = [tuple(v) + (0,) * (8 - len(v)) for v in variants]
+    variants = [tuple(v) + (0,) * (10 - len(v)) for v in variants]
     bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if args.dtype == "f64" else S.F32)
     ref = None
     res = {v: [] for v in variants}
@@ -85,7 +86,8 @@ def main():
                 T.spmm_hip_info(h, inf)
                 plan[v] = {"T": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]), "blocks": int(inf[5]),
                            "split_rows": int(inf[6]), "windows": int(inf[12]), "win_cols": int(inf[13]),
-                           "segments": int(inf[14])}
+                           "segments": int(inf[14]), "xcd": int(inf[15]), "lmax": int(inf[16]),
+                           "exact_rows": int(inf[17])}
                 out = Cm.clone()
                 if ref is None:
                     ref = out
