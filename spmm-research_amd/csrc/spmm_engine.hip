@@ -557,14 +557,16 @@ constexpr double VL_MIN_ROW = 32.0;   // mean virtual-row length (2 gather batch
 // every row in flight sweeps) plus the rows in flight themselves: in the default round-robin order every XCD sees
 // the rows in flight of the whole chip (~1024 resident workgroups x rows per block), in XCD order only its own
 // eighth.  The order pays when that eighth brings the working set under an L2 while the chip-wide one is well
-// above it: rows of span << rows in flight (400 K rows, bw 0.01, K=32: 0.172 -> 0.154 ms); for spans wider than
-// the rows in flight it costs 6-12 % (config 2 K=1/8/32; bw 0.05-0.3 K=1), so it is not used there.
+// above it -- rows of span << rows in flight (400 K rows, bw 0.01, K=32: 0.172 -> 0.154 ms) -- and only while all
+// of B fits the aggregate L2 (medium sample: B <= 17 MB 1.02-1.81x, e.g. 12 K rows K=128 0.125 -> 0.069 ms; B 35-57
+// MB 0.89-0.94x).  For spans wider than the rows in flight it costs 6-12 % (config 2 K=1/8/32; bw 0.05-0.3 K=1).
 constexpr double XCD_RESIDENT_BLOCKS = 1024.0;   // 256 CUs x 4 workgroups (VGPR-limited occupancy)
+constexpr double XCD_MAX_B_BYTES = 24.0 * (1 << 20);
 bool xcd_order(const spmm_hip_t *h, double srow, double span, int cap) {
     const int64_t env = env_int("SPMM_HIP_XCD", 0);
     const int64_t forced = h->var.xcd != 0 ? h->var.xcd : env;
     if (forced != 0) return forced > 0;
-    if (h->m < 8 * 64 || h->nnz == 0) return false;
+    if (h->m < 8 * 64 || h->nnz == 0 || (double)h->ncols * srow > XCD_MAX_B_BYTES) return false;
     const double avg = (double)h->nnz / (double)h->m;
     const double rows_per_block = std::min((double)CAP_ROWS, std::max(1.0, (double)cap / std::max(avg, 1.0)));
     const double in_flight = std::min((double)h->m, XCD_RESIDENT_BLOCKS * rows_per_block) * (double)h->ncols / (double)h->m;
