@@ -6,7 +6,8 @@
 //   * d_i ~ |N(avg, std)| ("normal", lib/random.h random_normal: Box-Muller) or Gamma(k=(avg/std)^2,
 //     theta=std^2/avg) ("gamma", Marsaglia-Tsang), rounded, capped at nr_cols.
 //   * skew > 0: one row (seeded choice) gets degree avg*(1+skew) (capped at nr_cols); the other rows are scaled so
-//     that the total stays avg*nr_rows -- the feature skew = (max - avg)/avg then equals the parameter.
+//     that the total stays avg*nr_rows and clamped at that degree -- the feature skew = (max - avg)/avg then equals
+//     the parameter even when it lies below the natural tail of the degree distribution.
 //   * neighbours: the row is laid out as R = d*(1 - nu/2) runs of consecutive columns separated by >= 1 free column;
 //     a run of length L contributes 2(L-1) to the row-neighbour count, so the mean over the row's nonzeros is nu.
 //   * columns live in a window of width W_i = bw*nr_cols*(R_t+1)/(R_t-1) centred on the diagonal, R_t = the row's
@@ -115,11 +116,30 @@ int row_degrees(const spmm_gen_params_t *p, std::vector<int64_t> &deg) {
             if (i != giant) rest += raw[i];
         const double want = std::max(0.0, avg * (double)m - (double)giant_deg);
         scale = rest > 0 ? want / rest : 0.0;
+        // the clamp at giant_deg removes mass from the tail: re-solve the scale (bisection, deterministic) so the
+        // clamped rows still sum to the wanted total
+        auto clamped_sum = [&](double sc) {
+            double t = 0;
+#pragma omp parallel for reduction(+ : t)
+            for (int64_t i = 0; i < m; ++i)
+                if (i != giant) t += (double)std::min<int64_t>((int64_t)std::llround(raw[i] * sc), giant_deg);
+            return t;
+        };
+        if (scale > 0 && clamped_sum(scale) < 0.999 * want) {
+            double lo = scale, hi = scale;
+            for (int it = 0; it < 8 && clamped_sum(hi) < want; ++it) hi *= 2.0;
+            for (int it = 0; it < 24; ++it) {
+                const double mid = 0.5 * (lo + hi);
+                (clamped_sum(mid) < want ? lo : hi) = mid;
+            }
+            scale = hi;
+        }
     }
     int64_t total = 0;
 #pragma omp parallel for reduction(+ : total)
     for (int64_t i = 0; i < m; ++i) {
         int64_t d = (i == giant) ? giant_deg : (int64_t)std::llround(raw[i] * scale);
+        if (giant >= 0) d = std::min(d, giant_deg);   // the heavy row IS the maximum (small skews: below the tail)
         d = std::max<int64_t>(0, std::min<int64_t>(d, n));
         deg[i] = d;
         total += d;
@@ -130,13 +150,14 @@ int row_degrees(const spmm_gen_params_t *p, std::vector<int64_t> &deg) {
 
 struct RowGen {
     const spmm_gen_params_t *p;
+    double bw_scale = 1.0;   // 1 / fraction of rows with >= 2 nonzeros (1-nonzero rows span nothing)
     std::vector<int32_t> prev, cur, tmp;
     std::vector<std::pair<int32_t, int32_t>> runs_prev, runs_cur;  // (start, length)
 
     // window [lo, lo+W) for row i with degree d laid out as rt independently placed runs
     void window(int64_t i, int64_t d, int64_t rt, int64_t &lo, int64_t &W) const {
         const int64_t n = p->nr_cols, m = p->nr_rows;
-        double w = p->bw * (double)n;
+        double w = p->bw * bw_scale * (double)n;
         if (rt >= 2) w *= (double)(rt + 1) / (double)(rt - 1);
         W = std::max<int64_t>(std::llround(w), std::max<int64_t>(1, d));
         // room for the runs and their separating gaps
@@ -191,8 +212,8 @@ struct RowGen {
         // their ends, otherwise R_t - copied new runs are placed in the row's own window.
         int64_t rest = d - (int64_t)cur.size();
         int64_t Rt = std::max<int64_t>(1, std::llround((double)d * (1.0 - nu / 2.0)));
-        if (p->bw * (double)n >= 2.0 * (double)d) {
-            const double bwf = std::min(0.95, p->bw);
+        if (p->bw * bw_scale * (double)n >= 2.0 * (double)d) {
+            const double bwf = std::min(0.95, p->bw * bw_scale);
             Rt = std::max<int64_t>(Rt, (int64_t)std::ceil((1.0 + bwf) / (1.0 - bwf) - 1e-9));
         }
         Rt = std::min<int64_t>(Rt, d);
@@ -292,10 +313,14 @@ int alloc_csr(spmm_csr_t *out, int64_t m, int64_t ncols, int64_t nnz) {
 void fill_rows(const spmm_gen_params_t *p, const std::vector<int64_t> &deg, int64_t r0, int64_t r1,
                spmm_csr_t *out) {
     const int64_t seg0 = r0 / SEG, seg1 = (r1 + SEG - 1) / SEG;
+    int64_t multi = 0;   // rows with >= 2 nonzeros, over the WHOLE matrix (same for every row range)
+    for (int64_t d : deg) multi += (d >= 2);
+    const double bw_scale = 1.0 / std::max(0.05, (double)multi / (double)std::max<size_t>(deg.size(), 1));
 #pragma omp parallel
     {
         RowGen g;
         g.p = p;
+        g.bw_scale = bw_scale;
 #pragma omp for schedule(dynamic, 1)
         for (int64_t s = seg0; s < seg1; ++s) {
             g.prev.clear();

@@ -48,7 +48,7 @@ def measure(line: str) -> dict:
     if req["skew"] > 0:
         err["skew"] = got["skew"] / min(req["skew"], cap) - 1.0
     else:
-        err["std"] = got["std"] / req["std"] - 1.0
+        err["std"] = got["std"] / req["std"] - 1.0 if req["std"] > 0 else got["std"] / max(req["avg"], 1e-12)
     return {"gen": line, "req": req, "got": got, "err": err}
 
 

@@ -26,10 +26,18 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tools"))
 
 
+def twin_names() -> dict:
+    """generator line -> name of the validation matrix it twins (reference config.sh:283-339)."""
+    d = json.loads((ROOT / "tools" / "validation_twins.json").read_text())["twins"]
+    return {line: name for name, line in d.items()}
+
+
 def dataset_lines(args) -> list[str]:
     if args.line:
         return list(args.line)
-    if args.dataset == "medium":
+    if args.dataset == "twins":
+        lines = list(json.loads((ROOT / "tools" / "validation_twins.json").read_text())["twins"].values())
+    elif args.dataset == "medium":
         from medium_dataset import medium_dataset_lines
         lines = medium_dataset_lines()
     else:
@@ -68,19 +76,48 @@ def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, exact):
             "long_rows_checked": int((~seq).sum())}
 
 
+def cpu_baseline(O, A, vals, x_col, k, budget_s, cores):
+    """Reference compute_csr (oracle/_ref, compiled from the reference's sources) on this host, same A and B:
+    1 warm-up + timed calls within budget_s (at least 1); median GFLOP/s.  Falls back to the C restatement."""
+    vt = "d" if vals.dtype == np.float64 else "f"
+    y = np.zeros(A.m * k, vals.dtype)
+    if O.ref_available(vt):
+        L = O.ref_lib(vt)
+        L.ref_set_threads(cores)
+        h = L.ref_create(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, k)
+        call = lambda: L.ref_run(h, x_col, y, k)  # noqa: E731
+        kind = "reference"
+    else:
+        call = lambda: O.spmm(A.row_ptr, A.col_idx, vals, A.ncols, x_col, k, cores)  # noqa: E731
+        kind = "port"
+    call()
+    ts = []
+    t_end = time.perf_counter() + budget_s
+    while not ts or (time.perf_counter() < t_end and len(ts) < 20):
+        t0 = time.perf_counter()
+        call()
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    return {"cpu_gflops": 2.0 * A.nnz * k / t / 1e9, "cpu_ms": t * 1e3, "cpu_calls": len(ts), "cpu_kind": kind,
+            "cpu_cores": cores}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--dataset", default="medium", help="'medium' or a path to a file of generator lines")
+    ap.add_argument("--dataset", default="medium",
+                    help="'medium', 'twins' (the 52 validation twins, tools/validation_twins.json) or a file of lines")
     ap.add_argument("--line", action="append", help="explicit generator line(s) instead of a dataset")
     ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--offset", type=int, default=0)
     ap.add_argument("--sort-by-size", action="store_true")
     ap.add_argument("--k", default="32")
-    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--dtype", default="f64", help="comma list of f64,f32")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--check-rows", type=int, default=256)
     ap.add_argument("--max-nnz", type=float, default=2.0e8)
+    ap.add_argument("--cpu-baseline", type=float, default=0.0,
+                    help="seconds of reference-CPU timing per (matrix, K, dtype); 0 = none")
     ap.add_argument("--budget", type=float, default=1e9, help="seconds; stop starting new matrices after this")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "sweep.jsonl"))
     args = ap.parse_args()
@@ -91,9 +128,10 @@ def main():
 
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
-    dtype = np.float64 if args.dtype == "f64" else np.float32
-    tdtype = torch.float64 if args.dtype == "f64" else torch.float32
+    dtypes = [d.strip() for d in args.dtype.split(",")]
     ks = [int(x) for x in args.k.split(",")]
+    names = twin_names() if args.dataset == "twins" else {}
+    cores = min(16, len(os.sched_getaffinity(0)))
     out = Path(args.out)
     out.parent.mkdir(parents=True, exist_ok=True)
     done = set()
@@ -107,7 +145,7 @@ def main():
     t_start = time.time()
     rng = np.random.default_rng(0)
     for li, line in enumerate(dataset_lines(args)):
-        todo = [k for k in ks if (line, k, args.dtype) not in done]
+        todo = [(dt, k) for dt in dtypes for k in ks if (line, k, dt) not in done]
         if not todo:
             continue
         if time.time() - t_start > args.budget:
@@ -120,41 +158,52 @@ def main():
         A = S.generate(p)
         t_gen = time.time() - t0
         feat = S.features(A)
-        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(dtype), A.m, A.ncols, A.nnz, 0, 0)
-        for k in todo:
-            mf.plan(k)
-            g = torch.Generator(device=dev)
-            g.manual_seed(42)
-            B = torch.rand((A.ncols, k), generator=g, device=dev, dtype=tdtype)
-            Cm = torch.empty((A.m, k), device=dev, dtype=tdtype)
-            run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
-            for _ in range(args.warmup):
-                run()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(args.iters):
-                run()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / args.iters
-            bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
-            par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows())
-            inf = mf.info()
-            rec = {"gen": line, "k": k, "dtype": args.dtype, "m": int(A.m), "nnz": int(A.nnz), "ms": ms,
-                   "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9, "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9,
-                   "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12, "mem_mb": feat["mem_footprint"],
-                   "features": {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled", "skew",
-                                                     "avg_num_neighbours", "cross_row_similarity")},
-                   "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]),
-                   "split_rows": int(inf[6]), "blocks": int(inf[5]), "windows": int(inf[12]),
-                   "win_cols": int(inf[13]), "segments": int(inf[14]), "xcd": int(inf[15]), "lmax": int(inf[16]),
-                   "exact_rows": int(inf[17]), **par}
-            with open(out, "a") as f:
-                f.write(json.dumps(rec) + "\n")
-            print(json.dumps({k2: rec[k2] for k2 in ("gen", "k", "ms", "gflops", "roofline_frac",
-                                                     "bitexact_seq_rows", "normwise_ok")}), flush=True)
-            del B, Cm
-        mf.close()
+        for dt in dtypes:
+            dtype = np.float64 if dt == "f64" else np.float32
+            tdtype = torch.float64 if dt == "f64" else torch.float32
+            vals = A.values.astype(dtype)
+            mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
+            for dt2, k in todo:
+                if dt2 != dt:
+                    continue
+                mf.plan(k)
+                g = torch.Generator(device=dev)
+                g.manual_seed(42)
+                B = torch.rand((A.ncols, k), generator=g, device=dev, dtype=tdtype)
+                Cm = torch.empty((A.m, k), device=dev, dtype=tdtype)
+                run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
+                for _ in range(args.warmup):
+                    run()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.iters):
+                    run()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / args.iters
+                bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
+                par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows())
+                inf = mf.info()
+                rec = {"gen": line, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m), "nnz": int(A.nnz),
+                       "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9, "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9,
+                       "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12, "mem_mb": feat["mem_footprint"],
+                       "features": {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled", "skew",
+                                                         "avg_num_neighbours", "cross_row_similarity")},
+                       "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]),
+                       "split_rows": int(inf[6]), "blocks": int(inf[5]), "windows": int(inf[12]),
+                       "win_cols": int(inf[13]), "segments": int(inf[14]), "xcd": int(inf[15]), "lmax": int(inf[16]),
+                       "exact_rows": int(inf[17]), **par}
+                if args.cpu_baseline > 0:
+                    x_col = np.ascontiguousarray(B.cpu().numpy().T).ravel()
+                    rec.update(cpu_baseline(O, A, vals, x_col, k, args.cpu_baseline, cores))
+                    rec["gpu_over_cpu"] = rec["gflops"] / rec["cpu_gflops"]
+                with open(out, "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+                print(json.dumps({k2: rec.get(k2) for k2 in ("name", "gen", "k", "dtype", "ms", "gflops",
+                                                             "roofline_frac", "cpu_gflops", "bitexact_seq_rows",
+                                                             "normwise_ok")}), flush=True)
+                del B, Cm
+            mf.close()
         del A
 
 
