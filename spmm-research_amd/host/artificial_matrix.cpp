@@ -271,6 +271,28 @@ struct RowGen {
             std::sort(cur.begin(), cur.end());
             cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
             // 3. top up after collisions: random free columns, window first, then the whole row
+            if (d - (int64_t)cur.size() > 4096) {
+                // many missing columns (a huge or dense row): a bitmap of the row instead of sorted inserts
+                // (quadratic); random free columns while the window is sparse, then free columns in window order
+                // from a random offset, then the rest of the row
+                std::vector<uint8_t> bm((size_t)n, 0);
+                for (int32_t c : cur) bm[(size_t)c] = 1;
+                int64_t have = (int64_t)cur.size();
+                for (int64_t guard = 0; have < d && guard < 8 * d; ++guard) {
+                    const int64_t c = lo + r.below(W);
+                    if (!bm[(size_t)c]) bm[(size_t)c] = 1, ++have;
+                }
+                const int64_t off = r.below(std::max<int64_t>(1, W));
+                for (int64_t t = 0; t < W && have < d; ++t) {
+                    const int64_t c = lo + (off + t) % W;
+                    if (!bm[(size_t)c]) bm[(size_t)c] = 1, ++have;
+                }
+                for (int64_t c = 0; c < n && have < d; ++c)
+                    if (!bm[(size_t)c]) bm[(size_t)c] = 1, ++have;
+                cur.clear();
+                for (int64_t c = 0; c < n; ++c)
+                    if (bm[(size_t)c]) cur.push_back((int32_t)c);
+            }
             int64_t guard = 0;
             while ((int64_t)cur.size() < d) {
                 const bool wide = guard++ > 64 * d;
