@@ -540,6 +540,8 @@ constexpr double WIN_MIN_SPAN_WIDE = 3.0;          // ... B rows >= 256 bytes (K
 constexpr double WIN_MIN_SEG = 48.0;               // mean nonzeros per segment at the chosen width
 constexpr double WIN_MIN_ROW_BYTES = 32.0;         // B row bytes: K=1..3 fp64 gathers are request-bound
 constexpr double WIN_LINE = 128.0;                 // L2 line
+constexpr double WIN_MIN_LAUNCH_NNZ = 1.0e6;       // nonzeros per window launch (~500 blocks: 4 K-row rail4284 in
+                                                   // 45 windows ran 120-block launches, 4x slower than one launch)
 
 // Window width in B bytes for a B row of srow bytes (measured best: 1-1.5 MB at K=8 fp64, 4-6 MB at K=32/128 fp64).
 double window_bytes(double srow) {
@@ -604,6 +606,8 @@ int64_t window_cols(const spmm_hip_t *h, int kw, const std::vector<Piece> &pcs, 
     const int64_t nseg = count_segments(pcs, col, W);
     *nseg_out = nseg;
     if (forced > 0) return W;
+    const double nwin = std::ceil((double)h->ncols / (double)W);
+    if ((double)h->nnz < WIN_MIN_LAUNCH_NNZ * nwin) return 0;
     return (double)h->nnz >= WIN_MIN_SEG * (double)nseg ? W : 0;
 }
 
@@ -825,22 +829,40 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         const double mean_vrow = nvr > 0 ? (double)h->nnz / nvr : 0.0;
         const int env_l = env_int("SPMM_HIP_LANES", 0);
         const int forced = h->var.lanes != 0 ? h->var.lanes : env_l;
+        bool all_blocks = false;
         if (forced != 0)
-            pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
+            all_blocks = forced > 0, pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
         else
-            pl.lmax = (h->nnz > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW) ? lcap : 1;
+            all_blocks = h->nnz > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW,
+            pl.lmax = all_blocks ? lcap : 1;
+        // flag the blocks that may use vector lanes: all of them under the policy, else (unless disabled) the blocks
+        // made only of split-row pieces (inexact anyway; a 16 M-nonzero row is thousands of one-piece blocks)
+        auto dest_of = [&](int v) -> int64_t {
+            if (in.vdest.empty()) return v;
+            return (W > 0) ? (in.vdest[v] >> 1) : in.vdest[v];
+        };
+        bool any_flag = false;
+        for (int2 &bk : in.blk) {
+            bool ok = all_blocks;
+            if (!ok && forced >= 0 && !in.long_rows.empty() && bk.y - bk.x < ng) {
+                ok = true;
+                for (int v = bk.x; v < bk.y && ok; ++v) ok = dest_of(v) < 0;
+            }
+            if (ok) bk.y |= BLK_VL_FLAG, any_flag = true;
+        }
+        if (any_flag && pl.lmax <= 1) pl.lmax = lcap;
         h->exact.assign((size_t)h->m, 1);
         for (const int4 &lr : in.long_rows) h->exact[(size_t)lr.x] = 0;
         if (pl.lmax > 1) {
             for (const int2 &bk : in.blk) {
-                const int nrows = bk.y - bk.x;
+                if (!(bk.y & BLK_VL_FLAG)) continue;
+                const int e = bk.y & BLK_ROWS_MASK, nrows = e - bk.x;
                 if (nrows >= ng) continue;
                 int L = 1;
                 while (2 * L <= ng / nrows) L *= 2;
                 if (std::min(L, pl.lmax) <= 1) continue;
-                for (int v = bk.x; v < bk.y; ++v) {
-                    int64_t d = v;
-                    if (!in.vdest.empty()) d = (W > 0) ? (in.vdest[v] >> 1) : in.vdest[v];
+                for (int v = bk.x; v < e; ++v) {
+                    const int64_t d = dest_of(v);
                     if (d >= 0) h->exact[(size_t)d] = 0;
                 }
             }

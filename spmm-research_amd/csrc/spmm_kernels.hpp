@@ -148,6 +148,8 @@ __device__ __forceinline__ void vshfl_add(vec<T, N> &acc, int off) {
 // XCD one contiguous eighth of the block table, i.e. of the rows, so an XCD's L2 only ever holds the B rows of its
 // own row range (speed only: any placement computes the same result).
 enum { DEST_ROW = 0, DEST_SPLIT = 1, DEST_CHAIN = 2 };
+constexpr int BLK_VL_FLAG = 1 << 30;          // blk[b].y: vector lanes allowed in this block
+constexpr int BLK_ROWS_MASK = BLK_VL_FLAG - 1;
 __device__ __forceinline__ int xcd_block(int w, int nb) {
     const int x = w & 7, i = w >> 3, q = nb >> 3, r = nb & 7;
     return x * q + (x < r ? x : r) + i;
@@ -157,10 +159,11 @@ __device__ __forceinline__ int xcd_block(int w, int nb) {
 // L = min(lmax, pow2floor(NG / rows)) groups; sub-lane l sums nonzeros l, l+L, ... and the L partials are added by a
 // fixed xor-shuffle tree.  Deterministic, within the 1e-10 normwise contract, but not the reference's single chain:
 // rows of blocks with L > 1 are reported as inexact (spmm_hip_exact_rows).  L is block-uniform; L = 1 blocks are
-// exactly the plain kernel.
+// exactly the plain kernel.  Only blocks flagged by the inspector (bit 30 of blk.y: all blocks when the matrix-wide
+// policy chose vector lanes, else blocks made only of split-row pieces, which are inexact anyway) may use L > 1.
 template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE, bool XCD = false,
           bool VL = false>
-__global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
+__global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
                                                        const int2 *__restrict__ blk, int nblk,
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int tid = threadIdx.x;
     const int2 rr = blk[b];
-    const int r0 = rr.x, r1 = rr.y;
+    const int r0 = rr.x, r1 = rr.y & BLK_ROWS_MASK;
     const int nrows = r1 - r0;
     const int j0 = vrow_ptr[r0];
     const int j1 = vrow_ptr[r1];
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
     const int lane = tid % G;
     int L = 1;
     if constexpr (VL) {
-        if (nrows < NG) {
+        if ((rr.y & BLK_VL_FLAG) && nrows < NG) {
             L = 1 << (31 - __builtin_clz(NG / nrows));
             L = L < lmax ? L : lmax;
         }
@@ -269,8 +272,8 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
             } else {
                 dst = C + (size_t)(r0 + r) * ld;
             }
-            if constexpr (VL) {
-                acc = row_dot_strided<T, VEC, U>(acc, s_col, s_val, s_rp[r] - jb + sub, s_rp[r + 1] - jb, L, gather);
+            if (VL && L > 1) {   // block-uniform branch: L = 1 blocks run the plain unit-stride chain below
+                acc = row_dot_strided<T, VEC, U / 2>(acc, s_col, s_val, s_rp[r] - jb + sub, s_rp[r + 1] - jb, L, gather);
                 for (int off = (G * L) >> 1; off >= G; off >>= 1) vshfl_add(acc, off);   // fixed tree over sub-lanes
                 if (sub == 0) vstore<T, VEC, NTC>(dst + kk, acc);
             } else {
@@ -284,7 +287,9 @@ __global__ __launch_bounds__(WG) void spmm_rows_kernel(const int32_t *__restrict
 // long_rows[b] = {row, first_slot, nslots, 0}: C[row][n] = sum of the row's partial slots P[first_slot + q][n].
 // One workgroup per split row: KW = min(pow2ceil(K), 64) columns per pass x SL = 256/KW slot lanes; slot lane l sums
 // slots l, l+SL, ... in order, then a fixed binary tree over the slot lanes in LDS (deterministic: the shape depends
-// only on nslots and K; O(nslots/SL + log SL) deep instead of a serial chain over all slots).
+// only on nslots and K; O(nslots/SL + log SL) deep instead of a serial chain over all slots).  Each slot lane keeps
+// CA independent accumulators (slot j of the lane into acc[j % CA], then added in order) so a row of thousands of
+// pieces (a 16 M-nonzero row: 8 K slots) keeps CA loads in flight instead of one dependent add per slot.
 template <typename T>
 __global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict__ long_rows,
                                                           const T *__restrict__ P, T *__restrict__ C, int K) {
@@ -296,9 +301,20 @@ __global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict
     const int n = threadIdx.x % kw, sl = threadIdx.x / kw;
     for (int c0 = 0; c0 < K; c0 += kw) {
         const int col = c0 + n;
-        T s = T(0);
-        if (col < K)
-            for (int q = sl; q < lr.z; q += sl_n) s += P[(size_t)(lr.y + q) * K + col];
+        constexpr int CA = 8;
+        T a[CA];
+#pragma unroll
+        for (int c = 0; c < CA; ++c) a[c] = T(0);
+        if (col < K) {
+            int q = sl, j = 0;
+            for (; q + (CA - 1) * sl_n < lr.z; q += CA * sl_n)
+#pragma unroll
+                for (int c = 0; c < CA; ++c) a[c] += P[(size_t)(lr.y + q + c * sl_n) * K + col];
+            for (; q < lr.z; q += sl_n, ++j) a[j] += P[(size_t)(lr.y + q) * K + col];
+        }
+        T s = a[0];
+#pragma unroll
+        for (int c = 1; c < CA; ++c) s += a[c];
         red[threadIdx.x] = s;
         __syncthreads();
         for (int w = sl_n / 2; w >= 1; w /= 2) {

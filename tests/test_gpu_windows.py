@@ -122,6 +122,7 @@ def test_policy_windows_dense_matrix(env, monkeypatch):
     k = 32
     x = O.drand48(3, A.ncols * k)
     monkeypatch.delenv("SPMM_HIP_WIN_BYTES", raising=False)
+    monkeypatch.setenv("SPMM_HIP_LANES", "-1")       # split-row pieces would get block-dependent lanes
     mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0)
     y = np.full(A.m * k, np.nan)
     mf.spmm(x, y, k)
