@@ -83,8 +83,15 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k);
 
 /* Timing of the LAST run on the handle, from HIP events recorded on the run's stream (blocks until the run
  * finished): out_ms[0] = SpMM kernel(s) only, out_ms[1] = B transpose (0 if none), out_ms[2] = H2D of x,
- * out_ms[3] = D2H of y (the last two only for spmm_hip_run). */
+ * out_ms[3] = D2H of y (the last two only for spmm_hip_run).  spmm_hip_run always records them; spmm_hip_run_device
+ * only after spmm_hip_set_timing(h, 1) (or with SPMM_HIP_EVENTS=1 at create): an event pair around every launch
+ * costs ~7.5 us of stream time per call on MI355X, so back-to-back callers that time the stream
+ * themselves leave it off (all zeros are returned then). */
 int spmm_hip_last_times(spmm_hip_t *h, double *out_ms);
+
+/* Statistics hook: replaces Matrix_Format::statistics_start (spmv_kernel.h:19, called before the timed loop at
+ * spmv_bench.cpp:350-352): on != 0 makes spmm_hip_run_device record the events spmm_hip_last_times reads. */
+int spmm_hip_set_timing(spmm_hip_t *h, int32_t on);
 
 /* Statistics: replaces statistics_print_labels / Matrix_Format::statistics_print_data
  * (spmv_kernel.h:20,30; spmv_bench.cpp:441-443,474-476).  Appends CSV columns to buf (at most buf_n bytes incl.
@@ -108,7 +115,8 @@ int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
  * row's nonzeros are dealt round-robin over L groups and the L partials added by a fixed tree -- deterministic,
  * within the 1e-10 normwise contract, not the single chain; SPMM_HIP_LANES=<n> / -1 force / disable),
  * out[17]=C rows computed as one left-to-right FMA chain (bit-identical to the reference; spmm_hip_exact_rows),
- * out[18..19]=reserved (0). */
+ * out[18]=1 when split rows are combined inside the row kernel (the block storing a row's last partial sums it:
+ * no combine launch; SPMM_HIP_FUSE=0 keeps the separate combine kernel), out[19]=reserved (0). */
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
 
 /* Which C rows of the current plan are computed as ONE left-to-right FMA chain over the row in CSR order -- the

@@ -108,11 +108,14 @@ struct spmm_hip_handle {
     int64_t nv = 0;                  // virtual rows
     int nblk = 0, nlong = 0, nslots = 0;
     int32_t *d_vrow_ptr = nullptr, *d_vdest = nullptr;
-    int2 *d_blk = nullptr;
+    int4 *d_blk = nullptr;           // {first, end | flags, vrow_ptr[first], vrow_ptr[end]} per block
     int4 *d_long_rows = nullptr;
     std::vector<int> win_blk;        // blocks of column window w: [win_blk[w], win_blk[w+1])
     std::vector<int64_t> win_v;      // virtual rows of column window w: [win_v[w], win_v[w+1])
     std::vector<uint8_t> exact;      // per C row: 1 = one left-to-right FMA chain (spmm_hip_exact_rows)
+    int32_t *d_lr_cnt = nullptr;     // fused combine: per split row, pieces stored so far in this launch (re-armed to 0)
+    int32_t *d_slot_lr = nullptr;    // fused combine: partial slot -> split row
+    bool fuse = false;               // split rows combined inside the row kernel (no spmm_combine_kernel launch)
     int32_t *d_wcol = nullptr;       // chained mode: col_idx / values in window-major segment order
     void *d_wval = nullptr;
 
@@ -127,6 +130,7 @@ struct spmm_hip_handle {
     hipStream_t stream = nullptr;  // own stream for spmm_hip_run
     hipEvent_t ev[8] = {};
     bool have_times = false, have_transpose = false, have_copies = false;
+    bool rec_events = false;         // run_device records timing events (spmm_hip_set_timing / SPMM_HIP_EVENTS=1)
     int64_t a_bytes = 0;
 };
 
@@ -159,12 +163,14 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 
 void free_plan(spmm_hip_t *h) {
     void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
-                  h->d_wcol, h->d_wval};
+                  h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
     h->d_wcol = nullptr;
     h->d_wval = nullptr;
+    h->d_lr_cnt = h->d_slot_lr = nullptr;
+    h->fuse = false;
     h->win_blk.clear();
     h->win_v.clear();
     h->d_vrow_ptr = h->d_vdest = nullptr;
@@ -189,17 +195,19 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
                 if (nb == 0) continue;
                 spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, DEST_CHAIN, false, decltype(vl_c)::value>
                     <<<nb, WG, 0, s>>>(h->d_vrow_ptr, h->d_wcol, (const T *)h->d_wval, h->d_blk + b0, nb, h->d_vdest,
-                                       B, C, P, ld, kw, bb, lmax);
+                                       B, C, P, ld, kw, bb, lmax, nullptr, nullptr, nullptr, 0u);
             }
         };
         if (lmax > 1) gow(std::true_type()); else gow(std::false_type());
         return;
     }
+    // partial slots of this panel as one buffer resource (the fused path needs them below 4 GiB; checked at plan)
+    const uint32_t pb = (uint32_t)std::min<uint64_t>((uint64_t)h->nslots * ld * sizeof(T), 0xFFFFFFFFull);
     auto go = [&](auto mode_c, auto xcd_c, auto vl_c) {
         spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
                          decltype(vl_c)::value><<<h->nblk, WG, 0, s>>>(
             h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
-            h->plan.lmax);
+            h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
     };
     using split_c = std::integral_constant<int, DEST_SPLIT>;
     using row_c = std::integral_constant<int, DEST_ROW>;
@@ -292,7 +300,7 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
             launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
         }
     }
-    if (h->nlong > 0) {
+    if (h->nlong > 0 && !h->fuse) {
         spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
     }
 }
@@ -735,6 +743,7 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
     h->a_bytes = (int64_t)(col_b + val_b);
     HIPCHK_C(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     for (auto &e : h->ev) HIPCHK_C(hipEventCreate(&e));
+    h->rec_events = env_int("SPMM_HIP_EVENTS", 0) != 0;
 #undef HIPCHK_C
     if (k > 0) {
         int st = spmm_hip_plan(h, k);
@@ -870,6 +879,43 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         pl.exact_rows = 0;
         for (uint8_t e : h->exact) pl.exact_rows += e;
     }
+    // fused combine: split rows summed by the block that stores their last piece, so no combine
+    // launch.  Needs one launch per panel (no column windows), partials below 4 GiB (32-bit buffer offsets) and each
+    // split row's pieces in consecutive virtual rows with consecutive slots (what inspect() builds; checked here).
+    // SPMM_HIP_FUSE=0 keeps the separate spmm_combine_kernel.
+    std::vector<int32_t> slot_lr;
+    {
+        bool fuse = h->nslots > 0 && W == 0 && env_int("SPMM_HIP_FUSE", 1) != 0 &&
+                    (uint64_t)h->nslots * (uint64_t)k * h->vsize < (1ULL << 32);
+        if (fuse) {
+            slot_lr.assign((size_t)h->nslots, -1);
+            std::vector<int64_t> slot_v((size_t)h->nslots, -1);
+            for (size_t v = 0; v < in.vdest.size(); ++v)
+                if (in.vdest[v] < 0) slot_v[(size_t)(-in.vdest[v] - 1)] = (int64_t)v;
+            for (size_t li = 0; li < in.long_rows.size() && fuse; ++li) {
+                const int4 lr = in.long_rows[li];
+                for (int q = 0; q < lr.z && fuse; ++q) {
+                    const int sl = lr.y + q;
+                    fuse = sl < h->nslots && slot_v[(size_t)sl] >= 0 && slot_lr[(size_t)sl] < 0 &&
+                           (q == 0 || slot_v[(size_t)sl] == slot_v[(size_t)sl - 1] + 1);
+                    if (fuse) slot_lr[(size_t)sl] = (int32_t)li;
+                }
+            }
+            for (int32_t x : slot_lr) fuse = fuse && x >= 0;
+        }
+        if (fuse) {
+            for (int2 &bk : in.blk) {
+                const int e = bk.y & BLK_ROWS_MASK;
+                for (int v = bk.x; v < e; ++v)
+                    if (in.vdest[(size_t)v] < 0) {
+                        bk.y |= BLK_SPLIT_FLAG;
+                        break;
+                    }
+            }
+        }
+        h->fuse = fuse;
+        if (!fuse) slot_lr.clear();
+    }
     h->plan = pl;
     h->win_blk = in.win_blk;
     h->win_v = in.win_v;
@@ -880,11 +926,23 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         return e;
     };
     hipError_t e = alloc_copy((void **)&h->d_vrow_ptr, in.vrow_ptr.data(), in.vrow_ptr.size() * 4);
-    if (e == hipSuccess) e = alloc_copy((void **)&h->d_blk, in.blk.data(), in.blk.size() * sizeof(int2));
+    {   // device block table carries the block's nonzero range too: one 16-B load instead of two dependent ones
+        std::vector<int4> blk4(in.blk.size());
+        for (size_t b = 0; b < in.blk.size(); ++b) {
+            const int2 bk = in.blk[b];
+            blk4[b] = make_int4(bk.x, bk.y, in.vrow_ptr[(size_t)bk.x], in.vrow_ptr[(size_t)(bk.y & BLK_ROWS_MASK)]);
+        }
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_blk, blk4.data(), blk4.size() * sizeof(int4));
+    }
     if (e == hipSuccess && !in.vdest.empty()) e = alloc_copy((void **)&h->d_vdest, in.vdest.data(), in.vdest.size() * 4);
     if (e == hipSuccess && h->nlong > 0)
         e = alloc_copy((void **)&h->d_long_rows, in.long_rows.data(), in.long_rows.size() * sizeof(int4));
-    h->insp_bytes = (in.vrow_ptr.size() + in.vdest.size()) * 4 + in.blk.size() * sizeof(int2) +
+    if (e == hipSuccess && h->fuse) {
+        e = alloc_copy((void **)&h->d_slot_lr, slot_lr.data(), slot_lr.size() * 4);
+        if (e == hipSuccess) e = hipMalloc((void **)&h->d_lr_cnt, (size_t)h->nlong * 4);
+        if (e == hipSuccess) e = hipMemset(h->d_lr_cnt, 0, (size_t)h->nlong * 4);
+    }
+    h->insp_bytes = (in.vrow_ptr.size() + in.vdest.size()) * 4 + in.blk.size() * sizeof(int4) +
                     in.long_rows.size() * sizeof(int4);
     h->b_bytes = (size_t)std::max<int64_t>(h->ncols, 1) * k * h->vsize;
     h->c_bytes = (size_t)std::max<int64_t>(h->m, 1) * k * h->vsize;
@@ -928,22 +986,23 @@ int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
     const void *B = d_b;
+    const bool ev = h->rec_events;
     h->have_transpose = false;
     if (b_layout == SPMM_HIP_B_COL_MAJOR) {
-        HIPCHK(hipEventRecord(h->ev[2], s));
+        if (ev) HIPCHK(hipEventRecord(h->ev[2], s));
         int st = launch_transpose(h, d_b, h->d_b, k, s);
         if (st != SPMM_HIP_OK) return st;
-        HIPCHK(hipEventRecord(h->ev[3], s));
+        if (ev) HIPCHK(hipEventRecord(h->ev[3], s));
         B = h->d_b;
-        h->have_transpose = true;
+        h->have_transpose = ev;
     }
-    HIPCHK(hipEventRecord(h->ev[0], s));
+    if (ev) HIPCHK(hipEventRecord(h->ev[0], s));
     if (h->m > 0) {
         int st = launch_spmm(h, B, d_c, k, s);
         if (st != SPMM_HIP_OK) return st;
     }
-    HIPCHK(hipEventRecord(h->ev[1], s));
-    h->have_times = true;
+    if (ev) HIPCHK(hipEventRecord(h->ev[1], s));
+    h->have_times = ev;
     h->have_copies = false;
     return SPMM_HIP_OK;
 }
@@ -979,6 +1038,12 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k) {
     HIPCHK(hipStreamSynchronize(s));
     h->last_x = x;
     h->have_times = h->have_transpose = h->have_copies = true;
+    return SPMM_HIP_OK;
+}
+
+int spmm_hip_set_timing(spmm_hip_t *h, int32_t on) {
+    if (!h) return fail(SPMM_HIP_ERR_ARG, "set_timing: handle is NULL");
+    h->rec_events = on != 0;
     return SPMM_HIP_OK;
 }
 
@@ -1047,7 +1112,8 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
     out[15] = h->plan.xcd;
     out[16] = h->plan.lmax;
     out[17] = h->plan.exact_rows;
-    out[18] = out[19] = 0;
+    out[18] = h->fuse ? 1 : 0;
+    out[19] = 0;
     return SPMM_HIP_OK;
 }
 

@@ -134,8 +134,9 @@ __device__ __forceinline__ void vshfl_add(vec<T, N> &acc, int off) {
 }
 
 // ------------------------------------------------------------------------------------------------ row blocks
-// blk[b] = {first, end}: the virtual rows of block b (<= CAP nonzeros in all, <= CAP_ROWS rows); blocks holding
-// long serial rows come first in the table (they start at time 0), the rest in row order.  vrow_ptr indexes
+// blk[b] = {first, end | flags, j0, j1}: the virtual rows of block b and their nonzero range (<= CAP nonzeros in
+// all, <= CAP_ROWS rows); blocks holding long serial rows come first in the table (they start at time 0), the rest
+// in row order.  vrow_ptr indexes
 // col_idx / values (the original arrays, or the window-major copy in chained mode).  B and C point at the panel's
 // first column; ld is their row stride (K); kw the panel width.  Destination of virtual row v by MODE:
 //   DEST_ROW   v IS C row v;
@@ -149,7 +150,84 @@ __device__ __forceinline__ void vshfl_add(vec<T, N> &acc, int off) {
 // own row range (speed only: any placement computes the same result).
 enum { DEST_ROW = 0, DEST_SPLIT = 1, DEST_CHAIN = 2 };
 constexpr int BLK_VL_FLAG = 1 << 30;          // blk[b].y: vector lanes allowed in this block
-constexpr int BLK_ROWS_MASK = BLK_VL_FLAG - 1;
+constexpr int BLK_SPLIT_FLAG = 1 << 29;       // blk[b].y: the block writes partial slots (fused combine, below)
+constexpr int BLK_ROWS_MASK = BLK_SPLIT_FLAG - 1;
+constexpr int CPOL_SC1 = 16;                  // buffer intrinsics' aux operand: sc1 (agent-coherent) on gfx950
+
+typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
+
+// 4/8/16-byte sc1 store (written through to the agent-coherent level: visible to sc1 loads of other XCDs once the
+// storing wave has waited vmcnt(0) -- MI355X_MICROARCH.md, inter-workgroup visibility, hand-off table row 1)
+template <typename T, int N>
+__device__ __forceinline__ void vstore_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, const vec<T, N> &v) {
+    constexpr int BYTES = (int)sizeof(T) * N;
+    static_assert(BYTES == 4 || BYTES == 8 || BYTES == 16, "sc1 store width");
+    if constexpr (BYTES == 16) {
+        i32x4 r;
+        __builtin_memcpy(&r, &v, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(r, rs, off, 0, CPOL_SC1);
+    } else if constexpr (BYTES == 8) {
+        i32x2 r;
+        __builtin_memcpy(&r, &v, 8);
+        __builtin_amdgcn_raw_buffer_store_b64(r, rs, off, 0, CPOL_SC1);
+    } else {
+        int32_t r;
+        __builtin_memcpy(&r, &v, 4);
+        __builtin_amdgcn_raw_buffer_store_b32(r, rs, off, 0, CPOL_SC1);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T load_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    T v;
+    if constexpr (sizeof(T) == 8) {
+        const i32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, CPOL_SC1);
+        __builtin_memcpy(&v, &r, 8);
+    } else {
+        const int32_t r = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, CPOL_SC1);
+        __builtin_memcpy(&v, &r, 4);
+    }
+    return v;
+}
+
+// Sum of a split row's partial slots: C[row][0..kw) = sum_q P[first_slot + q][0..kw) (row stride ld), by the whole
+// workgroup: KW = min(pow2ceil(kw), 64) columns per pass x SL = 256/KW slot lanes; slot lane l sums slots l, l+SL, ...
+// in order (CA independent accumulators, slot j of the lane into acc[j % CA], then added in order) so a row of
+// thousands of pieces keeps CA loads in flight; then a fixed binary tree over the slot lanes in LDS.  Deterministic:
+// the shape depends only on nslots and kw.  ldp(i) loads P element i.
+template <typename T, typename LoadP>
+__device__ __forceinline__ void combine_row(const int4 lr, T *__restrict__ C, int ld, int kw, T *red,
+                                            const LoadP &ldp) {
+    int KW = 1;
+    while (KW < kw && KW < 64) KW <<= 1;
+    const int sl_n = WG / KW;
+    const int n = threadIdx.x % KW, sl = threadIdx.x / KW;
+    for (int c0 = 0; c0 < kw; c0 += KW) {
+        const int col = c0 + n;
+        constexpr int CA = 8;
+        T a[CA];
+#pragma unroll
+        for (int c = 0; c < CA; ++c) a[c] = T(0);
+        if (col < kw) {
+            int q = sl, j = 0;
+            for (; q + (CA - 1) * sl_n < lr.z; q += CA * sl_n)
+#pragma unroll
+                for (int c = 0; c < CA; ++c) a[c] += ldp((size_t)(lr.y + q + c * sl_n) * ld + col);
+            for (; q < lr.z; q += sl_n, ++j) a[j] += ldp((size_t)(lr.y + q) * ld + col);
+        }
+        T s = a[0];
+#pragma unroll
+        for (int c = 1; c < CA; ++c) s += a[c];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = sl_n / 2; w >= 1; w /= 2) {
+            if (sl < w) red[threadIdx.x] += red[threadIdx.x + w * KW];
+            __syncthreads();
+        }
+        if (sl == 0 && col < kw) C[(size_t)lr.x * ld + col] = red[n];
+        __syncthreads();
+    }
+}
 __device__ __forceinline__ int xcd_block(int w, int nb) {
     const int x = w & 7, i = w >> 3, q = nb >> 3, r = nb & 7;
     return x * q + (x < r ? x : r) + i;
@@ -166,10 +244,13 @@ template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool B
 __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
-                                                       const int2 *__restrict__ blk, int nblk,
+                                                       const int4 *__restrict__ blk, int nblk,
                                                        const int32_t *__restrict__ vdest,
                                                        const T *__restrict__ B, T *__restrict__ C, T *__restrict__ P,
-                                                       int ld, int kw, uint32_t b_bytes, int lmax) {
+                                                       int ld, int kw, uint32_t b_bytes, int lmax,
+                                                       int32_t *__restrict__ lr_cnt,
+                                                       const int32_t *__restrict__ slot_lr,
+                                                       const int4 *__restrict__ long_rows, uint32_t p_bytes) {
     constexpr int SVN = 16 / (int)sizeof(T);
     constexpr int CAPP = CAP + 4;                         // staged window starts at a 16-byte boundary
     __shared__ __attribute__((aligned(16))) int32_t s_rp[CAP_ROWS + 64];
@@ -180,11 +261,13 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
 
     const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int tid = threadIdx.x;
-    const int2 rr = blk[b];
+    __shared__ int s_ndone;
+    if (tid == 0) s_ndone = 0;
+    const int4 rr = blk[b];                                 // {first, end | flags, vrow_ptr[first], vrow_ptr[end]}
     const int r0 = rr.x, r1 = rr.y & BLK_ROWS_MASK;
     const int nrows = r1 - r0;
-    const int j0 = vrow_ptr[r0];
-    const int j1 = vrow_ptr[r1];
+    const int j0 = rr.z;
+    const int j1 = rr.w;
 
     // Stage the block (col_idx / values from the 16-byte boundary jb <= j0 -- the device arrays are padded -- and the
     // virtual-row offsets).  DMA: LDS-DMA (global_load_lds, no VGPR destinations) in 1-KiB wave pieces of 16-byte
@@ -254,6 +337,11 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
     const int sub = (tid / G) % L;               // 0 when L = 1
     const int grp = tid / (G * L);
     const int rstep = NG / L;
+    // fused combine (DEST_SPLIT with lr_cnt): partial slots are stored sc1 and the block that completes a split row
+    // sums it (below), so no second launch
+    const bool fuse = MODE == DEST_SPLIT && lr_cnt != nullptr;
+    __amdgpu_buffer_rsrc_t prs;
+    if (MODE == DEST_SPLIT) prs = __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)p_bytes, 0x00020000);
     for (int kc = 0; kc < kw; kc += G * VEC) {
         const int kk = kc + lane * VEC;
         if (kk >= kw) continue;
@@ -261,9 +349,13 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
         for (int r = grp; r < nrows; r += rstep) {
             T *dst;
             V acc = vzero<T, VEC>();
+            bool sc1 = false;      // partial slot of a fused launch: sc1 store at byte offset poff of P
+            uint32_t poff = 0;
             if constexpr (MODE == DEST_SPLIT) {
                 const int d = vdest[r0 + r];
                 dst = (d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld;
+                sc1 = fuse && d < 0;
+                poff = (uint32_t)(((size_t)(-d - 1) * ld + kk) * sizeof(T));
             } else if constexpr (MODE == DEST_CHAIN) {
                 const int code = vdest[r0 + r];
                 const int d = code >> 1;
@@ -275,55 +367,58 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
             if (VL && L > 1) {   // block-uniform branch: L = 1 blocks run the plain unit-stride chain below
                 acc = row_dot_strided<T, VEC, U / 2>(acc, s_col, s_val, s_rp[r] - jb + sub, s_rp[r + 1] - jb, L, gather);
                 for (int off = (G * L) >> 1; off >= G; off >>= 1) vshfl_add(acc, off);   // fixed tree over sub-lanes
-                if (sub == 0) vstore<T, VEC, NTC>(dst + kk, acc);
+                if (sub == 0) {
+                    if (MODE == DEST_SPLIT && sc1) vstore_sc1<T, VEC>(prs, poff, acc);
+                    else vstore<T, VEC, NTC>(dst + kk, acc);
+                }
             } else {
                 acc = row_dot<T, VEC, U>(acc, s_col, s_val, s_rp[r] - jb, s_rp[r + 1] - jb, gather);
-                vstore<T, VEC, NTC>(dst + kk, acc);
+                if (MODE == DEST_SPLIT && sc1) vstore_sc1<T, VEC>(prs, poff, acc);
+                else vstore<T, VEC, NTC>(dst + kk, acc);
             }
+        }
+    }
+
+    if constexpr (MODE == DEST_SPLIT) {
+        // Fused combine.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): every partial is
+        // an sc1 store; every wave waits vmcnt(0), then a barrier; per split row touched, ONE lane adds this block's
+        // piece count to the row's agent-scope counter; the block whose add completes the count (told by the value
+        // its add returned) sums the row with sc1 loads after a barrier, and re-arms the counter for the next launch.
+        // The pieces of a split row are consecutive virtual rows with consecutive slots (checked by the host).
+        if (!fuse || !(rr.y & BLK_SPLIT_FLAG)) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int *s_done = s_rp;                    // s_rp / s_val are free after the barrier
+        for (int t = tid; t < nrows; t += WG) {
+            const int d = vdest[r0 + t];
+            if (d >= 0) continue;
+            const int sl = -d - 1;
+            const int li = slot_lr[sl];
+            const int4 lr = long_rows[li];
+            if (t > 0 && sl > lr.y && vdest[r0 + t - 1] == d + 1) continue;   // not the first piece of its run here
+            const int np = min(lr.y + lr.z - sl, nrows - t);
+            const int old = __hip_atomic_fetch_add(lr_cnt + li, np, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + np == lr.z) s_done[atomicAdd(&s_ndone, 1)] = li;
+        }
+        __syncthreads();
+        const int nd = s_ndone;
+        T *red = s_val;
+        for (int i = 0; i < nd; ++i) {
+            const int li = s_done[i];
+            combine_row<T>(long_rows[li], C, ld, kw, red,
+                           [&](size_t e) { return load_sc1<T>(prs, (uint32_t)(e * sizeof(T))); });
+            if (tid == 0) __hip_atomic_store(lr_cnt + li, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
 
 // long_rows[b] = {row, first_slot, nslots, 0}: C[row][n] = sum of the row's partial slots P[first_slot + q][n].
-// One workgroup per split row: KW = min(pow2ceil(K), 64) columns per pass x SL = 256/KW slot lanes; slot lane l sums
-// slots l, l+SL, ... in order, then a fixed binary tree over the slot lanes in LDS (deterministic: the shape depends
-// only on nslots and K; O(nslots/SL + log SL) deep instead of a serial chain over all slots).  Each slot lane keeps
-// CA independent accumulators (slot j of the lane into acc[j % CA], then added in order) so a row of thousands of
-// pieces (a 16 M-nonzero row: 8 K slots) keeps CA loads in flight instead of one dependent add per slot.
+// Separate combine launch (column-window plans, or partials beyond 4 GiB): one workgroup per split row.
 template <typename T>
 __global__ __launch_bounds__(WG) void spmm_combine_kernel(const int4 *__restrict__ long_rows,
                                                           const T *__restrict__ P, T *__restrict__ C, int K) {
     __shared__ T red[WG];
-    const int4 lr = long_rows[blockIdx.x];
-    int kw = 1;
-    while (kw < K && kw < 64) kw <<= 1;
-    const int sl_n = WG / kw;
-    const int n = threadIdx.x % kw, sl = threadIdx.x / kw;
-    for (int c0 = 0; c0 < K; c0 += kw) {
-        const int col = c0 + n;
-        constexpr int CA = 8;
-        T a[CA];
-#pragma unroll
-        for (int c = 0; c < CA; ++c) a[c] = T(0);
-        if (col < K) {
-            int q = sl, j = 0;
-            for (; q + (CA - 1) * sl_n < lr.z; q += CA * sl_n)
-#pragma unroll
-                for (int c = 0; c < CA; ++c) a[c] += P[(size_t)(lr.y + q + c * sl_n) * K + col];
-            for (; q < lr.z; q += sl_n, ++j) a[j] += P[(size_t)(lr.y + q) * K + col];
-        }
-        T s = a[0];
-#pragma unroll
-        for (int c = 1; c < CA; ++c) s += a[c];
-        red[threadIdx.x] = s;
-        __syncthreads();
-        for (int w = sl_n / 2; w >= 1; w /= 2) {
-            if (sl < w) red[threadIdx.x] += red[threadIdx.x + w * kw];
-            __syncthreads();
-        }
-        if (sl == 0 && col < K) C[(size_t)lr.x * K + col] = red[n];
-        __syncthreads();
-    }
+    combine_row<T>(long_rows[blockIdx.x], C, K, K, red, [&](size_t e) { return P[e]; });
 }
 
 

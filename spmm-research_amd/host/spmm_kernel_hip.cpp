@@ -42,7 +42,7 @@ struct HipCSR : Matrix_Format {
         int st = spmm_hip_run(h, x, y, k);
         if (st != SPMM_HIP_OK) die("spmm", st);
     }
-    void statistics_start() override {}
+    void statistics_start() override { spmm_hip_set_timing(h, 1); }
     int statistics_print_data(char *buf, long buf_n) override {
         int w = spmm_hip_stats(h, buf, buf_n);
         return w < 0 ? 0 : w;

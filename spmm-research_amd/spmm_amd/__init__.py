@@ -100,6 +100,7 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_run_device.argtypes = [vp, vp, i32, vp, i32, vp]
     L.spmm_hip_plan.argtypes = [vp, i32]
     L.spmm_hip_last_times.argtypes = [vp, _f64p]
+    L.spmm_hip_set_timing.argtypes = [vp, i32]
     L.spmm_hip_stats_labels.argtypes = [C.c_char_p, C.c_long]
     L.spmm_hip_stats.argtypes = [vp, C.c_char_p, C.c_long]
     L.spmm_hip_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
@@ -380,7 +381,8 @@ class MatrixFormat:
         return int(self.info()[8])
 
     def statistics_start(self) -> None:
-        pass
+        """Matrix_Format::statistics_start (spmv_kernel.h:19): later spmm_device calls record timing events."""
+        _check("set_timing", hip.spmm_hip_set_timing(self._h, 1))
 
     def statistics_print_data(self) -> str:
         buf = C.create_string_buffer(4096)

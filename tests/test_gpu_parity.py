@@ -151,6 +151,7 @@ def test_device_layouts_and_host_path_agree(env):
     Br = torch.from_numpy(x.reshape(k, A.ncols).T.copy()).to(dev)    # row-major [ncols][k]
     C1 = torch.empty((A.m, k), dtype=torch.float64, device=dev)
     C2 = torch.empty((A.m, k), dtype=torch.float64, device=dev)
+    mf.statistics_start()                                             # run_device records timing events from here
     mf.spmm_device(Xc.data_ptr(), S.B_COL_MAJOR, C1.data_ptr(), k, s)
     mf.spmm_device(Br.data_ptr(), S.B_ROW_MAJOR, C2.data_ptr(), k, s)
     torch.cuda.synchronize()
