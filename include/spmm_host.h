@@ -6,6 +6,8 @@
  *                           conversion + coo_to_csr(..., sort_columns=1, transpose=0)
  *                           (lib/storage_formats/matrix_market/matrix_market.c:249-314,
  *                            matrix_market_gen.c:70-158; spmv_bench.cpp:724-763,805-826; csr_gen.c:163-217)
+ *   spmm_host_smtx_read     smtx_read (DLMC .smtx: lib/storage_formats/dlcm_matrices/dlcm_matrix.c:152-324) + the
+ *                           harness's USE_DLCM_MATRICES copy (spmv_bench.cpp:667-696,769-801)
  *   spmm_host_coo_to_csr    coo_to_csr (lib/storage_formats/csr/csr_gen.c:163-217)
  *   spmm_host_generate      artificial_matrix_generation(nr_rows, nr_cols, avg, std, distribution, seed,
  *                           placement, bw, skew, avg_num_neighbours, cross_row_similarity)
@@ -88,6 +90,11 @@ int spmm_host_features(const spmm_csr_t *a, spmm_features_t *f);
 /* .mtx -> CSR (indexing identical to mtx_read + coo_to_csr).  field_out receives the header field
  * ("real", "integer", "complex", "pattern"), symmetric_out 0/1/2 (general/symmetric-or-Hermitian/skew). */
 int spmm_host_mtx_read(const char *path, spmm_csr_t *out, char *field_out, int field_n, int32_t *symmetric_out);
+
+/* DLMC .smtx -> CSR (smtx_read + the harness copy, lib/storage_formats/dlcm_matrices/dlcm_matrix.c:152-324,
+ * spmv_bench.cpp:667-696,769-801): row offsets and column indices used as stored (no sort); the format has no
+ * values, so they are a seeded uniform [-1, 1) stream (the reference's are time-seeded rand(), unreproducible). */
+int spmm_host_smtx_read(const char *path, int64_t value_seed, spmm_csr_t *out);
 
 int spmm_host_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t nnz,
                          int32_t *row_ptr, int32_t *col_idx, double *values);

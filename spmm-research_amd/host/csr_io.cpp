@@ -218,4 +218,58 @@ int spmm_host_mtx_read(const char *path, spmm_csr_t *out, char *field_out, int f
     return SPMM_HOST_OK;
 }
 
+// DLMC .smtx (lib/storage_formats/dlcm_matrices/dlcm_matrix.c:152-255 header, dlcm_matrix_gen.c:56-123 body):
+//   line 1  "M, K, nnz"            (sscanf "%ld,%ld,%ld")
+//   line 2  M+1 row offsets        (whitespace-separated; the CSR row_ptr, used as is)
+//   line 3  nnz column indices     (0-based, used as is: the harness copies them without coo_to_csr,
+//                                   spmv_bench.cpp:769-801, so rows keep the file's column order)
+// The format carries no values: the reference draws U(-1, 1) from rand() re-seeded with time(NULL) + j + thread
+// (dlcm_matrix_gen.c:111-122), i.e. not reproducible; here they are a seeded uniform [-1, 1) stream
+// (spmm_host_uniform_fill(value_seed, -1, 1)).  The reference parses without checks; malformed offsets or
+// out-of-range columns are rejected here (SPMM_HOST_ERR_PARSE).
+int spmm_host_smtx_read(const char *path, int64_t value_seed, spmm_csr_t *out) {
+    if (!path || !out) return SPMM_HOST_ERR_ARG;
+    memset(out, 0, sizeof(*out));
+    Lines L;
+    int st = read_lines(path, L);
+    if (st) return st;
+    if (L.start.empty()) return SPMM_HOST_ERR_PARSE;
+    long long M = 0, K = 0, NZ = 0;
+    if (sscanf(&L.buf[L.start[0]], "%lld,%lld,%lld", &M, &K, &NZ) != 3) return SPMM_HOST_ERR_PARSE;
+    if (M < 0 || K < 0 || NZ < 0) return SPMM_HOST_ERR_PARSE;
+    if (M >= INT32_MAX || K >= INT32_MAX || NZ >= INT32_MAX) return SPMM_HOST_ERR_OVERFLOW;
+    if (L.start.size() < (NZ > 0 ? 3u : 2u)) return SPMM_HOST_ERR_PARSE;
+    out->row_ptr = (int32_t *)malloc((size_t)(M + 1) * sizeof(int32_t));
+    out->col_idx = (int32_t *)malloc((size_t)std::max<long long>(NZ, 1) * sizeof(int32_t));
+    out->values = (double *)malloc((size_t)std::max<long long>(NZ, 1) * sizeof(double));
+    if (!out->row_ptr || !out->col_idx || !out->values) {
+        spmm_host_csr_free(out);
+        return SPMM_HOST_ERR_NOMEM;
+    }
+    // n integers from one line; fails on a short line or a token that is not a number
+    auto parse_ints = [](char *s, long long n, long long lo, long long hi, int32_t *dst) -> bool {
+        for (long long j = 0; j < n; ++j) {
+            char *end;
+            const long long v = strtoll(s, &end, 10);
+            if (end == s || v < lo || v > hi) return false;
+            dst[j] = (int32_t)v;
+            s = end;
+        }
+        return true;
+    };
+    bool ok = parse_ints(&L.buf[L.start[1]], M + 1, 0, NZ, out->row_ptr) && out->row_ptr[0] == 0 &&
+              out->row_ptr[M] == NZ;
+    for (long long i = 0; ok && i < M; ++i) ok = out->row_ptr[i] <= out->row_ptr[i + 1];
+    if (ok && NZ > 0) ok = parse_ints(&L.buf[L.start[2]], NZ, 0, K - 1, out->col_idx);
+    if (!ok) {
+        spmm_host_csr_free(out);
+        return SPMM_HOST_ERR_PARSE;
+    }
+    out->m = M;
+    out->ncols = K;
+    out->nnz = NZ;
+    spmm_host_uniform_fill(value_seed, -1.0, 1.0, out->values, NZ);
+    return SPMM_HOST_OK;
+}
+
 }  // extern "C"

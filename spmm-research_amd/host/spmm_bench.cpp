@@ -3,7 +3,8 @@
 // Keeps the reference harness contract (benchmark_code/CPU/AMD/spmv_code_bench/spmv_bench.cpp:564-1035) so the
 // existing run scripts drive it unchanged:
 //   env   NUM_COLS (= K), USE_ARTIFICIAL_MATRICES (0 = argv[1] is a .mtx path, 1 = argv holds the 11 generator
-//         parameters), USE_PROCESSES (fork replicas: not supported, must be 0), COOLDOWN
+//         parameters), USE_DLCM_MATRICES (1 = argv[1] is a DLMC .smtx path; values seeded U[-1,1)),
+//         USE_PROCESSES (fork replicas: not supported, must be 0), COOLDOWN
 //   argv  none -> print the CSV labels and exit (:606-610); a path; or 11 generator fields [+ name] (:851-868)
 //   out   log lines on stdout, ONE CSV row on stderr (:478 / :555), the accuracy report on stdout (:187-203)
 //   flow  x = B = 1.0 (:901), y = 0 (:907), csr_to_format (:996), 100 warm-up spmm calls (:316-320), timed calls
@@ -88,7 +89,9 @@ int main(int argc, char **argv) {
         matrix_name = argv[1];
         char field[32] = {0};
         int sym = 0;
-        int st = spmm_host_mtx_read(argv[1], &A, field, sizeof(field), &sym);
+        // USE_DLCM_MATRICES=1: argv[1] is a DLMC .smtx file, used as stored (spmv_bench.cpp:667-696,769-801)
+        int st = env_long("USE_DLCM_MATRICES", 0) != 0 ? spmm_host_smtx_read(argv[1], 42, &A)
+                                                        : spmm_host_mtx_read(argv[1], &A, field, sizeof(field), &sym);
         if (st) {
             fprintf(stderr, "error reading '%s' (status %d)\n", argv[1], st);
             return EXIT_FAILURE;

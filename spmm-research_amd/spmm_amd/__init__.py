@@ -129,6 +129,7 @@ def _bind_host(L: C.CDLL) -> C.CDLL:
     L.spmm_host_generate_rows.argtypes = [C.POINTER(_GenParams), i64, i64, C.POINTER(_CSRStruct)]
     L.spmm_host_features.argtypes = [C.POINTER(_CSRStruct), C.POINTER(_Features)]
     L.spmm_host_mtx_read.argtypes = [C.c_char_p, C.POINTER(_CSRStruct), C.c_char_p, C.c_int, C.POINTER(C.c_int32)]
+    L.spmm_host_smtx_read.argtypes = [C.c_char_p, i64, C.POINTER(_CSRStruct)]
     L.spmm_host_coo_to_csr.argtypes = [_i32p, _i32p, vp, i64, i64, _i32p, _i32p, _f64p]
     L.spmm_host_csr_free.argtypes = [C.POINTER(_CSRStruct)]
     L.spmm_host_drand48_fill.argtypes = [i64, _f64p, i64]
@@ -234,6 +235,16 @@ def mtx_read(path: str | os.PathLike) -> tuple[CSR, str, int]:
     if st != 0:
         raise ValueError(f"cannot read {path} (status {st})")
     return _take_csr(s), field.value.decode(), sym.value
+
+
+def smtx_read(path: str | os.PathLike, value_seed: int = 42) -> CSR:
+    """DLMC .smtx -> CSR as the reference harness uses it (offsets and columns as stored, no sort); values are a
+    seeded U[-1, 1) stream (the format has none; the reference's are time-seeded)."""
+    s = _CSRStruct()
+    st = host.spmm_host_smtx_read(os.fsencode(str(path)), value_seed, C.byref(s))
+    if st != 0:
+        raise ValueError(f"cannot read {path} (status {st})")
+    return _take_csr(s)
 
 
 def coo_to_csr(R, Cc, V, m: int) -> CSR:

@@ -277,3 +277,28 @@ def test_harness_executable_on_mtx(env):
     assert r.returncode == 0, r.stderr
     assert r.stderr.strip().splitlines()[-1].startswith("synthetic,normal,random,14,20000,20000,")
     assert "failing entries=0" in r.stdout
+
+
+def test_dlmc_smtx_unsorted_rows(env, tmp_path):
+    """DLMC input (USE_DLCM_MATRICES): the CSR is used as stored, so rows may be unsorted and hold duplicates;
+    the engine must still follow CSR order bit for bit (windows are never used on unsorted rows), and the harness
+    must read the .smtx and pass its accuracy check (negative values: the normwise criterion)."""
+    torch, S, O = env
+    rng = np.random.default_rng(11)
+    m, n = 3000, 2500
+    deg = rng.integers(0, 60, m)
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    ci = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    f = tmp_path / "dlmc.smtx"
+    f.write_text(f"{m}, {n}, {len(ci)}\n" + " ".join(map(str, rp)) + "\n" + " ".join(map(str, ci)) + "\n")
+    A = S.smtx_read(f)
+    for k in (1, 32):
+        x = O.drand48(5 + k, n * k)
+        y, ex = gpu_spmm(S, A.row_ptr, A.col_idx, A.values, m, n, x, k, want_exact=True)
+        check_split_aware(O, A.row_ptr, A.col_idx, A.values, n, x, k, y, ex, TOL_F64)
+    exe = ROOT / "spmm-research_amd" / "bin" / "spmm_csr_hip_d.exe"
+    envv = dict(os.environ, NUM_COLS="32", USE_ARTIFICIAL_MATRICES="0", USE_DLCM_MATRICES="1", SPMM_WARMUP="3",
+                SPMM_TIMED_LOOPS="5", SPMM_B_RANDOM="1")
+    r = subprocess.run([str(exe), str(f)], capture_output=True, text=True, env=envv, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "failing entries=0" in r.stdout

@@ -44,6 +44,46 @@ def test_mtx_reader_rejects_malformed(tmp_path):
         S.mtx_read(bad)
 
 
+def write_smtx(path, rp, ci, m, n):
+    """DLMC .smtx text as the reference reader expects it (dlcm_matrix.c:223, dlcm_matrix_gen.c:82-106)."""
+    path.write_text(f"{m}, {n}, {len(ci)}\n" + " ".join(map(str, rp)) + "\n" + " ".join(map(str, ci)) + "\n")
+
+
+def test_smtx_reader_keeps_stored_csr(tmp_path):
+    """USE_DLCM_MATRICES path: offsets and columns used exactly as stored (no coo_to_csr, no column sort),
+    values a seeded U[-1, 1) stream.  No .smtx fixture exists in the reference, so the round trip is synthetic."""
+    rng = np.random.default_rng(3)
+    m, n = 37, 53
+    deg = rng.integers(0, 9, m)
+    deg[5] = 0
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    ci = rng.integers(0, n, int(rp[-1])).astype(np.int32)       # unsorted rows, duplicates allowed
+    f = tmp_path / "a.smtx"
+    write_smtx(f, rp, ci, m, n)
+    A = S.smtx_read(f, value_seed=7)
+    assert (A.m, A.ncols, A.nnz) == (m, n, int(rp[-1]))
+    assert np.array_equal(A.row_ptr, rp) and np.array_equal(A.col_idx, ci)
+    assert np.array_equal(A.values, S.uniform(7, -1.0, 1.0, A.nnz))
+    assert np.array_equal(S.smtx_read(f, value_seed=7).values, A.values)
+    e = tmp_path / "empty.smtx"
+    e.write_text("4, 6, 0\n0 0 0 0 0\n")
+    E = S.smtx_read(e)
+    assert (E.m, E.ncols, E.nnz) == (4, 6, 0) and np.array_equal(E.row_ptr, np.zeros(5, np.int32))
+
+
+@pytest.mark.parametrize("text", ["3 3 2\n0 1 2 2\n0 1\n",         # header without commas
+                                  "3, 3, 2\n0 1 2\n0 1\n",          # short offsets line
+                                  "3, 3, 2\n0 2 1 2\n0 1\n",        # decreasing offsets
+                                  "3, 3, 2\n0 1 2 3\n0 1\n",        # last offset != nnz
+                                  "3, 3, 2\n0 1 2 2\n0 3\n",        # column out of range
+                                  "3, 3, 2\n0 1 2 2\n0\n"])         # short column line
+def test_smtx_reader_rejects_malformed(tmp_path, text):
+    f = tmp_path / "bad.smtx"
+    f.write_text(text)
+    with pytest.raises(ValueError):
+        S.smtx_read(f)
+
+
 def test_mtx_array_format(tmp_path):
     f = tmp_path / "dense.mtx"
     f.write_text("%%MatrixMarket matrix array real general\n2 3\n1\n2\n3\n4\n5\n6\n")
