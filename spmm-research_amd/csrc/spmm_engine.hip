@@ -550,6 +550,18 @@ constexpr double WIN_MIN_ROW_BYTES = 32.0;         // B row bytes: K=1..3 fp64 g
 constexpr double WIN_LINE = 128.0;                 // L2 line
 constexpr double WIN_MIN_LAUNCH_NNZ = 1.0e6;       // nonzeros per window launch (~500 blocks: 4 K-row rail4284 in
                                                    // 45 windows ran 120-block launches, 4x slower than one launch)
+// Tiny B rows (K = 1..2 fp64, srow <= 16 B): a gather fetches a whole line for 8-16 useful bytes while continuing
+// a chain into the next window costs a 2*srow C round trip, so windows pay even at ~1 nonzero per segment -- but
+// only for sparse rows whose span holds more B than 1.5 L2s and while there are few windows (each launch runs a
+// slice of every row) and consecutive rows do not share columns: measured (profiles/r01_s22_k1_windows,
+// r01_s23_tiny_windows) 1.14-1.25x at 3-10 windows of 4 MB (1.4-4.8 M rows, bw 0.6, crs 0.05), 0.84-0.91x at
+// 26-36 windows, config 2 (span 2.4 MB at K=1) 0.83x, crs 0.5-0.95 rows 0.6-0.76x.
+constexpr double WIN_TINY_ROW_BYTES = 16.0;
+constexpr double WIN_TINY_BYTES = 4.0 * (1 << 20);
+constexpr double WIN_TINY_MAX_WINDOWS = 12.0;
+constexpr double WIN_TINY_MAX_ROW = 32.0;          // mean row length (longer rows: vector lanes instead)
+constexpr double WIN_TINY_MAX_CRS = 0.25;          // similar consecutive rows already share their lines in L1/L2:
+                                                   // windows cost 0.6-0.76x there (medium sample, crs 0.5-0.95)
 
 // Window width in B bytes for a B row of srow bytes (measured best: 1-1.5 MB at K=8 fp64, 4-6 MB at K=32/128 fp64).
 double window_bytes(double srow) {
@@ -595,16 +607,65 @@ double mean_row_span(const int32_t *rp, const int32_t *col, int64_t m) {
     return n > 0 ? sum / (double)n : 0.0;
 }
 
+// Consecutive-row similarity on a sample of row pairs: mean over rows r (non-empty, with a non-empty row r+1) of the
+// fraction of r's nonzeros that have one within +-1 column in row r+1 -- the reference feature extractor's
+// cross_row_similarity (csr_util_gen.c:553-610) on <= 8192 evenly spaced rows.  High similarity means a row's B
+// rows were just gathered by its neighbour (L1/L2 hits); low means every nonzero gathers a fresh B row.
+double row_similarity_sample(const int32_t *rp, const int32_t *col, int64_t m) {
+    const int64_t ns = std::min<int64_t>(8192, m - 1);
+    double sum = 0.0;
+    int64_t n = 0;
+    std::vector<int32_t> a, b;
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t r = i * (m - 1) / std::max<int64_t>(ns, 1);
+        const int64_t la = rp[r + 1] - rp[r], lb = rp[r + 2] - rp[r + 1];
+        if (la == 0 || lb == 0 || la > 4096 || lb > 4096) continue;
+        a.assign(col + rp[r], col + rp[r + 1]);
+        b.assign(col + rp[r + 1], col + rp[r + 2]);
+        std::sort(a.begin(), a.end());
+        std::sort(b.begin(), b.end());
+        int64_t hit = 0;
+        size_t q = 0;
+        for (int32_t c : a) {
+            while (q < b.size() && b[q] < c - 1) ++q;
+            hit += (q < b.size() && b[q] <= c + 1);
+        }
+        sum += (double)hit / (double)la;
+        ++n;
+    }
+    return n > 0 ? sum / (double)n : 0.0;
+}
+
+// 128-byte K panels for gather-bound rows without cross-row reuse (measured, DESIGN §6.6, profiles/r01_s21_*): with
+// 256-B B rows every nonzero of a low-similarity row gathers a fresh row, and when the rows' span holds 4-12 L2s of
+// B, halving the B row halves that working set and the extra A pass is cheaper than the L2 misses it saves
+// (1.06-1.25x on 1.5 M x 100 bw 0.05, 1.8 M x 20 bw 0.05, 389 K x 50 bw 0.3 at K=32 and K=128); wider or narrower
+// spans, similar rows (crs >= 0.5: 0.75-0.9x) and short rows lose.
+constexpr double NARROW_MAX_CRS = 0.25;
+constexpr double NARROW_MIN_SPAN_L2 = 4.0, NARROW_MAX_SPAN_L2 = 12.0;
+constexpr double NARROW_MIN_ROW = 20.0;
+
 int64_t window_cols(const spmm_hip_t *h, int kw, const std::vector<Piece> &pcs, const int32_t *col,
-                    int64_t win_bytes_var, int64_t *nseg_out) {
+                    int64_t win_bytes_var, double crs, int64_t *nseg_out) {
     *nseg_out = 0;
     const double srow = (double)kw * (double)h->vsize;
     const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
     const int64_t forced = win_bytes_var != 0 ? win_bytes_var : env_bytes;
     if (forced < 0 || h->nnz == 0 || h->ncols < 2) return 0;
-    const double wb = forced > 0 ? (double)forced : window_bytes(srow);
+    const bool tiny = srow <= WIN_TINY_ROW_BYTES;
+    const double wb = forced > 0 ? (double)forced : tiny ? WIN_TINY_BYTES : window_bytes(srow);
     const int64_t W = std::max<int64_t>(1, (int64_t)(wb / srow));
     if (W >= h->ncols) return 0;
+    if (forced == 0 && tiny) {
+        const double nwin = std::ceil((double)h->ncols / (double)W);
+        const double avg = (double)h->nnz / (double)std::max<int64_t>(h->m, 1);
+        if (nwin > WIN_TINY_MAX_WINDOWS || avg >= WIN_TINY_MAX_ROW || crs >= WIN_TINY_MAX_CRS ||
+            (double)h->nnz < WIN_MIN_LAUNCH_NNZ * nwin ||
+            mean_row_span(h->h_row_ptr.data(), col, h->m) * srow < WIN_MIN_SPAN_NARROW * WIN_L2_BYTES)
+            return 0;
+        *nseg_out = count_segments(pcs, col, W);
+        return W;
+    }
     if (forced == 0) {
         if (srow < WIN_MIN_ROW_BYTES) return 0;
         const double min_span = srow <= 128.0 ? WIN_MIN_SPAN_NARROW : WIN_MIN_SPAN_WIDE;
@@ -775,6 +836,23 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     } else if (b_bytes > PANEL_MIN_B_BYTES && avg_row >= PANEL_MIN_ROW_NNZ) {
         pl.kw = std::min(k, std::max(1, (int)(PANEL_ROW_BYTES / h->vsize)));
     }
+    // col_idx on the host (span, row similarity, windows, XCD order) when some policy below may need it
+    std::vector<int32_t> hcol;
+    double span = (double)h->ncols, crs = 1.0;
+    auto load_cols = [&]() -> int {
+        if (!hcol.empty() || h->nnz == 0) return SPMM_HIP_OK;
+        hcol.resize((size_t)h->nnz);
+        HIPCHK(hipMemcpy(hcol.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
+        span = mean_row_span(h->h_row_ptr.data(), hcol.data(), h->m);
+        crs = row_similarity_sample(h->h_row_ptr.data(), hcol.data(), h->m);
+        return SPMM_HIP_OK;
+    };
+    if (h->var.panel_k <= 0 && panel_env <= 0 && (double)pl.kw * h->vsize == 2.0 * WIN_LINE &&
+        avg_row >= NARROW_MIN_ROW && h->m > 1) {
+        if (int st = load_cols()) return st;
+        const double x = span * 2.0 * WIN_LINE / WIN_L2_BYTES;
+        if (crs < NARROW_MAX_CRS && x >= NARROW_MIN_SPAN_L2 && x <= NARROW_MAX_SPAN_L2) pl.kw /= 2;
+    }
     pl.npanels = (k + pl.kw - 1) / pl.kw;
     // block capacity and split length
     int vec, g;
@@ -791,25 +869,22 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     // col_idx on the host
     Inspection in;
     int64_t W = 0;
-    std::vector<int32_t> hcol;
     {
         const double srow = (double)pl.kw * (double)h->vsize;
         const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
         const int64_t forced = h->var.win_bytes != 0 ? h->var.win_bytes : env_bytes;
         const bool b_big = (double)h->ncols * std::max(srow, WIN_LINE) > WIN_MIN_SPAN_NARROW * WIN_L2_BYTES;
-        const bool maybe_win = h->nnz > 0 && forced >= 0 && (forced > 0 || (b_big && srow >= WIN_MIN_ROW_BYTES));
+        const bool maybe_win = h->nnz > 0 && forced >= 0 && (forced > 0 || (b_big && (srow >= WIN_MIN_ROW_BYTES || srow <= WIN_TINY_ROW_BYTES)));
         const bool maybe_xcd = h->nnz > 0 && (double)h->ncols * srow > WIN_L2_BYTES;
         if (maybe_win || maybe_xcd) {
-            hcol.resize((size_t)h->nnz);
-            HIPCHK(hipMemcpy(hcol.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
+            if (int st = load_cols()) return st;
         }
-        const double span = hcol.empty() ? (double)h->ncols : mean_row_span(h->h_row_ptr.data(), hcol.data(), h->m);
         pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
         if (maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
             std::vector<Piece> pcs;
             Inspection tmp;
             make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
-            W = window_cols(h, pl.kw, pcs, hcol.data(), h->var.win_bytes, &pl.nseg);
+            W = window_cols(h, pl.kw, pcs, hcol.data(), h->var.win_bytes, crs, &pl.nseg);
         }
     }
     if (W > 0) {
