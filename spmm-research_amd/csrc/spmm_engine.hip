@@ -561,7 +561,8 @@ constexpr double WIN_TINY_BYTES = 4.0 * (1 << 20);
 constexpr double WIN_TINY_MAX_WINDOWS = 12.0;
 constexpr double WIN_TINY_MAX_ROW = 32.0;          // mean row length (longer rows: vector lanes instead)
 constexpr double WIN_TINY_MAX_CRS = 0.25;          // similar consecutive rows already share their lines in L1/L2:
-                                                   // windows cost 0.6-0.76x there (medium sample, crs 0.5-0.95)
+                                                   // windows cost 0.6-0.76x there (profiles/r01_s23_tiny_windows/
+                                                   // sweep_s160_k12_ungated.jsonl, crs 0.5-0.95)
 
 // Window width in B bytes for a B row of srow bytes (measured best: 1-1.5 MB at K=8 fp64, 4-6 MB at K=32/128 fp64).
 double window_bytes(double srow) {
