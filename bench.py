@@ -218,6 +218,9 @@ def main():
             "hbm_gbs_alg": round(achieved, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         # PMC bytes per launch moved in the measured launch time: what the L2-miss stream actually
+                         # sustains (the B gather re-fetches rows beyond L2)
+                         "traffic_gbs": None if traffic is None else round(traffic / (kern_ms * 1e-3) / 1e9, 1),
                          "bytes_alg_per_launch": bytes_launch, "kernel_ms_per_launch": round(kern_ms, 5),
                          "kernel_ms_max_over_ranks": round(kern_max_ms, 5)},
             "cpu_baseline": cpu,
