@@ -50,8 +50,16 @@ def parse():
 
 
 def engine_sha256() -> str:
+    """Fingerprint of the engine build: its device/host sources and the Makefile (flags), so PMC numbers collected for
+    one engine version stay attached to it across rebuilds (the .so bytes themselves are not reproducible: hipcc
+    embeds build paths)."""
     import hashlib
-    return hashlib.sha256((ROOT / "spmm-research_amd" / "lib" / "libspmm_hip.so").read_bytes()).hexdigest()
+    h = hashlib.sha256()
+    pkg = ROOT / "spmm-research_amd"
+    for f in (pkg / "csrc" / "spmm_engine.hip", pkg / "csrc" / "spmm_kernels.hpp", ROOT / "include" / "spmm_hip.h",
+              pkg / "Makefile"):
+        h.update(f.read_bytes())
+    return h.hexdigest()
 
 
 def cpu_baseline(A, k: int, budget_s: float) -> dict | None:
