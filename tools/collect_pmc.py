@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--gen", default=None)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--timeout", type=int, default=240)
+    ap.add_argument("--no-latest", action="store_true",
+                    help="do not overwrite profiles/pmc_latest.json (the bench line's traffic source, config 2 only)")
     args = ap.parse_args()
     bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--k", str(args.k)]
     if args.gen:
@@ -84,6 +86,7 @@ def main():
     import spmm_amd as S
     nnz = int(S.generate_row_ptr(S.gen_params(gen))[-1])
     summary = {"workload": gen, "k": args.k, "dtype": "f64", "kernel": KERNEL, "nnz": nnz,
+               "dispatches_counted": res.get("FETCH_SIZE", {}).get("dispatches"),
                "engine_sha256": bench.engine_sha256(),
                "counters_per_launch": {k: v["mean"] for k, v in res.items()},
                "hbm_bytes_per_launch": hbm,
@@ -96,7 +99,8 @@ def main():
     prof.mkdir(exist_ok=True)
     text = json.dumps(summary, indent=1)
     (prof / f"pmc_{args.tag}.json").write_text(text)
-    (prof / "pmc_latest.json").write_text(text)
+    if not args.no_latest:
+        (prof / "pmc_latest.json").write_text(text)
     (ROOT / "gpurun_out" / f"pmc_{args.tag}.json").write_text(text)
     print(text)
 
