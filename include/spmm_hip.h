@@ -73,7 +73,12 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
 /* Execute, device buffers (kernel-only path; graph-capturable: no allocation or synchronisation inside once the
  * handle is planned for this k and layout).  d_b: device B in `b_layout` (COL_MAJOR is transposed into an
  * internal row-major buffer first, as a separate kernel); d_c: device C row-major [m][k].  stream: a hipStream_t
- * (NULL = the null stream). */
+ * (NULL = the null stream).
+ * Concurrency: a handle owns per-run device scratch (the transposed B, split-row partial slots and their arrival
+ * counters), so calls on ONE handle must be serialised on ONE stream (as the reference's plugin is not reentrant,
+ * SURVEY §8b).  Two runs of the same handle in flight on different streams race on that scratch; use one handle
+ * per stream instead.  A COL_MAJOR run overwrites the internal B, so it also invalidates the upload cache of
+ * spmm_hip_run (SPMM_HIP_ASSUME_X_UNCHANGED). */
 int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *d_c, int32_t k, void *stream);
 
 /* Plan for k without running: the inspector (lane layout, block capacity, split length T, K panels of 256-byte B

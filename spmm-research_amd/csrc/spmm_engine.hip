@@ -1065,6 +1065,9 @@ int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *
     const bool ev = h->rec_events;
     h->have_transpose = false;
     if (b_layout == SPMM_HIP_B_COL_MAJOR) {
+        // h->d_b is about to hold THIS B: a later spmm_hip_run(x) must not skip its upload on the strength of
+        // SPMM_HIP_ASSUME_X_UNCHANGED (its cached x is no longer what d_b holds)
+        h->last_x = nullptr;
         if (ev) HIPCHK(hipEventRecord(h->ev[2], s));
         int st = launch_transpose(h, d_b, h->d_b, k, s);
         if (st != SPMM_HIP_OK) return st;

@@ -380,10 +380,17 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
     }
 
     if constexpr (MODE == DEST_SPLIT) {
-        // Fused combine.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): every partial is
-        // an sc1 store; every wave waits vmcnt(0), then a barrier; per split row touched, ONE lane adds this block's
-        // piece count to the row's agent-scope counter; the block whose add completes the count (told by the value
-        // its add returned) sums the row with sc1 loads after a barrier, and re-arms the counter for the next launch.
+        // Fused combine.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility), ordering spelled out:
+        //   producer  every partial is an sc1 (write-through) store -> every wave waits vmcnt(0) -> workgroup barrier
+        //             -> per split row touched, ONE lane adds this block's piece count to the row's agent-scope
+        //             counter.  No release fence: the payload never sits dirty in an L2 (sc1), so buffer_wbl2 would
+        //             only write back unrelated lines (the guide's "(2) without an agent release").
+        //   consumer  the block whose add completes the count (told by the value its add returned) -> barrier ->
+        //             agent-scope ACQUIRE fence (buffer_inv sc1: this CU's L1 holds no stale partial line) ->
+        //             vmcnt(0) -> barrier -> sc1 loads of the partials; then it re-arms the counter.
+        // The acquire makes the consumer side independent of the sc1-load-only argument, which the guide has
+        // measured for one workgroup per CU only (this kernel runs up to four).  It costs ~2 us per completing block
+        // and runs only in blocks that complete a split row.
         // The pieces of a split row are consecutive virtual rows with consecutive slots (checked by the host).
         if (!fuse || !(rr.y & BLK_SPLIT_FLAG)) return;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -402,6 +409,10 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
         }
         __syncthreads();
         const int nd = s_ndone;
+        if (nd == 0) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         T *red = s_val;
         for (int i = 0; i < nd; ++i) {
             const int li = s_done[i];

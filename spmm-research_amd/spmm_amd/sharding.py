@@ -9,9 +9,10 @@
 * C: stays sharded during the timed steps; ``allgather_rows`` assembles it (variable row counts, padded
   all_gather) for validation only.
 
-Weak scaling (bench.py): the global problem for N ranks is N stacked copies of the single-GPU shape -- N*m rows,
-N*ncols columns, bw/N so each row keeps the same absolute column window -- so every shard is statistically the
-one-GPU workload.
+Strong scaling (bench.py default, config 4): ONE global matrix (the generator line as given) split N ways -- the
+same problem at every N.  Weak scaling (bench.py --scaling weak): the global problem for N ranks is N stacked
+copies of the single-GPU shape -- N*m rows, N*ncols columns, bw/N so each row keeps the same absolute column
+window -- so every shard is statistically the one-GPU workload.
 """
 from __future__ import annotations
 
@@ -41,6 +42,11 @@ def weak_scaled_params(gen_line: str, world: int):
     p.nr_cols = p.nr_cols * world
     p.bw = p.bw / world
     return p
+
+
+def strong_params(gen_line: str):
+    """The global matrix of a strong-scaling run: the generator line unchanged at every N."""
+    return gen_params(gen_line)
 
 
 def make_shard(params, world: int, rank: int) -> Shard:

@@ -124,7 +124,7 @@ def test_validation_twins_fidelity():
     fall short: row degrees are drawn independently, so a short row cannot follow a long one; measured worst -0.27)."""
     import json
     from generator_fidelity import measure
-    tw = json.loads((ROOT / "tools" / "validation_twins.json").read_text())["twins"]
+    tw = json.loads((ROOT / "spmm-research_amd" / "spmm_amd" / "validation_twins.json").read_text())["twins"]
     assert len(tw) >= 52
     for name, line in tw.items():
         S.gen_params(line)                               # parses (raises otherwise)

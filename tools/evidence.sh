@@ -3,7 +3,7 @@
 # profiles/pmc_latest.json on the box so the bench line below carries it), bench line, rocprofv3 kernel-trace summary.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${1:-r01_v8}
+TAG=${1:?usage: tools/evidence.sh <tag>}
 OUT=gpurun_out/final
 mkdir -p $OUT
 export TMPDIR=/tmp

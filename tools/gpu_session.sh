@@ -21,7 +21,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 }
 WHAT=${1:-all}
 if [[ $WHAT == all || $WHAT == tests ]]; then
-    step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+    step pytest_gpu 1500 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
     step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $WHAT == all || $WHAT == bench ]]; then

@@ -1,71 +1,10 @@
-#!/usr/bin/env python3
-"""tools/medium_dataset.py -- the 11-field generator lines of synthetic_matrices_medium_dataset (BASELINE config 3).
-
-Regenerated from the dataset's published recipe (reference matrix_generation_parameters/create_param_file.py:4-68:
-three memory ranges 4-32 / 32-512 / 512-2048 MB with 5 sizes each, rows = floor((size*2^20 - 4) / (12*avg + 4)),
-std = round(avg/3, 4), normal/random, seed 14) with the grid the published file uses (avg {5,10,20,50,100,500},
-bw {0.05,0.3,0.6}, skew {0,100,1000,10000}, neighbours {0.05,0.5,0.95,1.4,1.9}, crs {0.05,0.5,0.95}).  The
-published file holds the same lines as a set minus the 10 listed in OMITTED (the tail of the grid); the sorted set's
-sha256 is pinned in tests/test_sweep_tools.py.  Only the recipe is restated here -- no data file is copied.
-"""
-from __future__ import annotations
-
-import hashlib
+"""Compatibility shim: the dataset recipes live in the package (spmm_amd/datasets.py)."""
 import sys
+from pathlib import Path
 
-MEM_RANGES = ["4-32", "32-512", "512-2048"]
-PER_RANGE = 5
-AVGS = [5, 10, 20, 50, 100, 500]
-BWS = [0.05, 0.3, 0.6]
-SKEWS = [0, 100, 1000, 10000]
-NEIGHS = [0.05, 0.5, 0.95, 1.4, 1.9]
-CRSS = [0.05, 0.5, 0.95]
-SEED = 14
-OMITTED = {
-    "303884 303884 500 166.6667 normal random 0.6 10000 1.4 0.95 14",
-    "303884 303884 500 166.6667 normal random 0.6 10000 1.9 0.05 14",
-    "303884 303884 500 166.6667 normal random 0.6 10000 1.9 0.5 14",
-    "303884 303884 500 166.6667 normal random 0.6 10000 1.9 0.95 14",
-    "4191 4191 500 166.6667 normal random 0.6 10000 1.9 0.05 14",
-    "4191 4191 500 166.6667 normal random 0.6 10000 1.9 0.5 14",
-    "4191 4191 500 166.6667 normal random 0.6 10000 1.9 0.95 14",
-    "72652 72652 500 166.6667 normal random 0.6 10000 1.9 0.05 14",
-    "72652 72652 500 166.6667 normal random 0.6 10000 1.9 0.5 14",
-    "72652 72652 500 166.6667 normal random 0.6 10000 1.9 0.95 14",
-}
-SHA256_SORTED = "c2c07be3a6d28819b294fa13ca62174056d62121d6f36a2922361cc2d39881c0"
-
-
-def _std(avg: float) -> str:
-    v = round(avg / 3, 4)          # numpy.round(avg / 3, 4) in the recipe; same digits for this grid
-    return repr(v)
-
-
-def medium_dataset_lines() -> list[str]:
-    out: list[str] = []
-    seen: set[str] = set()
-    for mr in MEM_RANGES:
-        lo, hi = (int(x) for x in mr.split("-"))
-        step = int((hi - lo) / PER_RANGE)
-        sizes = [i - 1 for i in range(lo + 1, hi, step)][:PER_RANGE]
-        for size in sizes:
-            for avg in AVGS:
-                rows = int((size * (1024 * 1024) - 4) // (12 * avg + 4))
-                for bw in BWS:
-                    for sk in SKEWS:
-                        for ne in NEIGHS:
-                            for cr in CRSS:
-                                line = " ".join(str(x) for x in
-                                                [rows, rows, avg, _std(avg), "normal", "random", bw, sk, ne, cr, SEED])
-                                if line not in seen and line not in OMITTED:
-                                    seen.add(line)
-                                    out.append(line)
-    return out
-
-
-def sorted_sha256(lines: list[str]) -> str:
-    return hashlib.sha256("\n".join(sorted(lines)).encode()).hexdigest()
-
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "spmm-research_amd"))
+from spmm_amd.datasets import *  # noqa: F401,F403,E402
+from spmm_amd.datasets import SHA256_SORTED, medium_dataset_lines, sorted_sha256  # noqa: F401,E402
 
 if __name__ == "__main__":
     L = medium_dataset_lines()

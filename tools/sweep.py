@@ -28,7 +28,7 @@ sys.path.insert(0, str(ROOT / "tools"))
 
 def twin_names() -> dict:
     """generator line -> name of the validation matrix it twins (reference config.sh:283-339)."""
-    d = json.loads((ROOT / "tools" / "validation_twins.json").read_text())["twins"]
+    d = json.loads((ROOT / "spmm-research_amd" / "spmm_amd" / "validation_twins.json").read_text())["twins"]
     return {line: name for name, line in d.items()}
 
 
@@ -36,7 +36,7 @@ def dataset_lines(args) -> list[str]:
     if args.line:
         return list(args.line)
     if args.dataset == "twins":
-        lines = list(json.loads((ROOT / "tools" / "validation_twins.json").read_text())["twins"].values())
+        lines = list(json.loads((ROOT / "spmm-research_amd" / "spmm_amd" / "validation_twins.json").read_text())["twins"].values())
     elif args.dataset == "medium":
         from medium_dataset import medium_dataset_lines
         lines = medium_dataset_lines()
@@ -105,7 +105,7 @@ def cpu_baseline(O, A, vals, x_col, k, budget_s, cores):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="medium",
-                    help="'medium', 'twins' (the 52 validation twins, tools/validation_twins.json) or a file of lines")
+                    help="'medium', 'twins' (the 52 validation twins, spmm_amd/validation_twins.json) or a file of lines")
     ap.add_argument("--line", action="append", help="explicit generator line(s) instead of a dataset")
     ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--offset", type=int, default=0)
