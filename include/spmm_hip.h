@@ -121,8 +121,17 @@ int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
  * within the 1e-10 normwise contract, not the single chain; SPMM_HIP_LANES=<n> / -1 force / disable),
  * out[17]=C rows computed as one left-to-right FMA chain (bit-identical to the reference; spmm_hip_exact_rows),
  * out[18]=1 when split rows are combined inside the row kernel (the block storing a row's last partial sums it:
- * no combine launch; SPMM_HIP_FUSE=0 keeps the separate combine kernel), out[19]=reserved (0). */
+ * no combine launch; SPMM_HIP_FUSE=0 keeps the separate combine kernel), out[19]=LDS B tiles (0 = none; see
+ * spmm_hip_tile_info). */
 int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
+
+/* LDS B tiles of the current plan: runs of up to 64 consecutive rows whose union of columns is
+ * read several times (similar or dense rows) are computed by a second kernel that stages each B row of the union
+ * in LDS once; every tile row is still one left-to-right FMA chain in CSR order (exact).  out has 6 slots:
+ * out[0]=tiles, out[1]=rows in tiles, out[2]=nonzeros in tiles, out[3]=chunks (LDS fills), out[4]=the sampled
+ * mean reuse (nonzeros per union column) x 1000 the policy decided on, out[5]=1 when tiles run in XCD order.
+ * SPMM_HIP_TILES=-1 disables tiles, =1 takes every eligible tile; SPMM_HIP_TILE_REUSE=<x> sets the threshold. */
+int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out);
 
 /* Which C rows of the current plan are computed as ONE left-to-right FMA chain over the row in CSR order -- the
  * reference kernel's exact operation sequence, so bit-identical to it (mask[i] = 1); the others (rows longer than
@@ -160,6 +169,30 @@ typedef struct {
 int spmm_hip_debug_inspect(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
                            int32_t cap, int64_t win_cols, spmm_hip_inspection_t *out);
 void spmm_hip_debug_free(spmm_hip_inspection_t *ins);
+
+/* Diagnostics (host only): the tile decomposition for a CSR pattern with sorted rows (tests).  Rows of at most T
+ * nonzeros are grouped in runs of up to rmax; a run becomes a tile when its reuse is >= min_reuse; its union of
+ * columns is cut into chunks of <= uc columns and <= capa entries (incl. padding); a run whose union exceeds colmax
+ * columns or that would make more than dmax chunks is halved until it fits (colmax / dmax <= 0: no limit).  Arrays malloc'ed, release with
+ * spmm_hip_debug_tiles_free:
+ *   tiles[4*ntile]       {first row, rows, first chunk, chunks}
+ *   chunks[4*(nchunk+1)] {first tcol, columns, first position, first tseg} (+ sentinel)
+ *   tcol[ncol]           union columns, chunk by chunk
+ *   tseg[nseg]           per chunk, rows+1 segment starts relative to the chunk's first position (8-aligned);
+ *                        every row segment is padded to a multiple of 4 entries
+ *   perm[nz], tlidx[nz]  position -> original nonzero (-1 = padding) and chunk-local column (0xFFFF = padding)
+ *   in_tile[m]           1 for rows in a tile */
+typedef struct {
+    int64_t ntile, nchunk, ncol, nseg, nz, m;
+    int32_t *tiles, *chunks, *tcol;
+    uint16_t *tseg, *tlidx;
+    int64_t *perm;
+    uint8_t *in_tile;
+} spmm_hip_tiles_t;
+int spmm_hip_debug_tiles(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
+                         int32_t rmax, int32_t uc, int32_t capa, double min_reuse, int32_t colmax, int32_t dmax,
+                         spmm_hip_tiles_t *out);
+void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t);
 
 const char *spmm_hip_strerror(int status);
 const char *spmm_hip_last_error_detail(void);

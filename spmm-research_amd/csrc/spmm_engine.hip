@@ -52,6 +52,16 @@ int fail(int status, const std::string &what) {
 
 constexpr int CAP = 2048;         // LDS capacity of a block (nonzeros)
 constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may read up to 3 elements past nnz)
+// LDS B tiles (spmm_tile_kernel)
+constexpr int TILE_UCB = 12 * 1024;       // LDS bytes of staged B rows per chunk (two chunk buffers per workgroup)
+constexpr int TILE_CAPA = 896;            // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
+constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
+constexpr double TILE_MIN_REUSE = 12.0;   // policy: sampled reuse (nnz per union column) to leave the row kernel
+                                          // (measured, DESIGN §6.9: 1.22x at ~14 on 39 K x 500 bw 0.05; 0.66-0.82x
+                                          // at 4.5-6; the kernel is LDS-throughput bound)
+constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
+constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value +0, the zero B row)
+constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
 
 // Production kernel variant (tools/tune_kernel.py on MI355X).
 #ifndef DEF_U
@@ -79,6 +89,10 @@ struct Plan {
     int xcd = 0;               // 1 = XCD-contiguous block order (each XCD sweeps one eighth of the rows)
     int lmax = 1;              // vector lanes: max groups per row (1 = every row one group, exact)
     int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
+    int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
+    int tile_xcd = 0;          // tiles in XCD-contiguous order
+    int64_t tile_rows = 0, tile_nnz = 0, tile_chunks = 0;
+    double tile_reuse = 0.0;   // sampled mean reuse (nnz per union column) the policy saw
 };
 
 struct Variant {
@@ -88,6 +102,7 @@ struct Variant {
     int64_t win_bytes = 0;     // 0 = inspector policy, < 0 = no column windows, > 0 = window of this many B bytes
     int xcd = 0;               // 0 = inspector policy, < 0 = off, > 0 = XCD-contiguous block order
     int lanes = 0;             // 0 = inspector policy, < 0 = off (exact rows), > 0 = vector lanes up to this many
+    int tiles = 0;             // 0 = inspector policy, < 0 = off, > 0 = every eligible tile with reuse >= 1
 };
 
 }  // namespace
@@ -118,6 +133,11 @@ struct spmm_hip_handle {
     bool fuse = false;               // split rows combined inside the row kernel (no spmm_combine_kernel launch)
     int32_t *d_wcol = nullptr;       // chained mode: col_idx / values in window-major segment order
     void *d_wval = nullptr;
+    int4 *d_tiles = nullptr, *d_tchunk = nullptr;   // tile mode (spmm_tile_kernel)
+    int32_t *d_tcol = nullptr;
+    uint16_t *d_tseg = nullptr, *d_tlidx = nullptr;
+    void *d_tval = nullptr;
+    long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
 
     // per-k buffers
     void *d_b = nullptr;      // row-major B [ncols][k]
@@ -163,13 +183,19 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 
 void free_plan(spmm_hip_t *h) {
     void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
-                  h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr};
+                  h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr, h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg,
+                  h->d_tlidx, h->d_tval, h->d_tstamps};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
     h->d_wcol = nullptr;
     h->d_wval = nullptr;
     h->d_lr_cnt = h->d_slot_lr = nullptr;
+    h->d_tiles = h->d_tchunk = nullptr;
+    h->d_tcol = nullptr;
+    h->d_tseg = h->d_tlidx = nullptr;
+    h->d_tval = nullptr;
+    h->d_tstamps = nullptr;
     h->fuse = false;
     h->win_blk.clear();
     h->win_v.clear();
@@ -213,7 +239,7 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     using row_c = std::integral_constant<int, DEST_ROW>;
     using T_ = std::true_type;
     using F_ = std::false_type;
-    const bool vl = h->plan.lmax > 1, sp = h->nslots > 0;
+    const bool vl = h->plan.lmax > 1, sp = h->d_vdest != nullptr;   // split rows, or rows left to tiles
     if (h->plan.xcd) {
         if (sp) vl ? go(split_c(), T_(), T_()) : go(split_c(), T_(), F_());
         else vl ? go(row_c(), T_(), T_()) : go(row_c(), T_(), F_());
@@ -290,15 +316,41 @@ void launch_panel(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStre
     }
 }
 
+// Tile kernel for a panel: 16-byte lanes (checked at plan), G lanes per row group, tile_rpg(G) rows per group.
+template <typename T, int G>
+void launch_tiles_g(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s) {
+    constexpr int VEC = 16 / (int)sizeof(T);
+    constexpr int NG = WG / G;
+    constexpr int RPG = NG * 8 <= TILE_RMAX ? 8 : (TILE_RMAX / NG > 1 ? TILE_RMAX / NG : 1);
+    auto go = [&](auto xcd_c) {
+        spmm_tile_kernel<T, VEC, G, RPG, TILE_UCB, TILE_CAPA, (bool)DEF_NTC, decltype(xcd_c)::value>
+            <<<h->plan.ntile, WG, 0, s>>>(h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg, (const T *)h->d_tval,
+                                           h->d_tlidx, B, C, ld, h->d_tstamps);
+    };
+    if (h->plan.tile_xcd) go(std::true_type()); else go(std::false_type());
+}
+
+template <typename T>
+void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s) {
+    int vec, g;
+    lane_layout(kw, ld, sizeof(T), vec, g);
+    switch (g) {
+        case 4: launch_tiles_g<T, 4>(h, B, C, ld, kw, s); break;     // (B rows >= 64 bytes: G >= 4, checked at plan)
+        case 8: launch_tiles_g<T, 8>(h, B, C, ld, kw, s); break;
+        case 16: launch_tiles_g<T, 16>(h, B, C, ld, kw, s); break;
+        case 32: launch_tiles_g<T, 32>(h, B, C, ld, kw, s); break;
+        default: launch_tiles_g<T, 64>(h, B, C, ld, kw, s); break;
+    }
+}
+
 template <typename T>
 void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     T *P = (T *)h->d_part;
-    if (h->nblk > 0) {
-        for (int p = 0; p < h->plan.npanels; ++p) {
-            const int k0 = p * h->plan.kw;
-            const int kw = std::min(h->plan.kw, K - k0);
-            launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
-        }
+    for (int p = 0; p < h->plan.npanels; ++p) {
+        const int k0 = p * h->plan.kw;
+        const int kw = std::min(h->plan.kw, K - k0);
+        if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
+        if (h->plan.ntile > 0) launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
     }
     if (h->nlong > 0 && !h->fuse) {
         spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
@@ -395,13 +447,26 @@ void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap
 }
 
 // Virtual rows (rows longer than T cut into T-nonzero pieces) packed into blocks (one column window).
-void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool heavy_first = true) {
+// skip (optional): rows computed elsewhere (tiles).  A run of skipped rows becomes one GAP virtual row (destination
+// 0, never in a block) so the virtual-row offsets stay one prefix array; blocks never cross a gap.
+void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool heavy_first = true,
+             const uint8_t *skip = nullptr) {
     out = Inspection();
     out.vrow_ptr.reserve((size_t)m + 1);
     out.vrow_ptr.push_back(rp[0]);
     bool any_split = false;
+    std::vector<int64_t> gaps;     // virtual-row index of each gap
     for (int64_t r = 0; r < m; ++r) {
         const int64_t len = (int64_t)rp[r + 1] - rp[r];
+        if (skip && skip[r]) {
+            int64_t r1 = r;
+            while (r1 < m && skip[r1]) ++r1;
+            gaps.push_back((int64_t)out.vrow_ptr.size() - 1);
+            out.vrow_ptr.push_back(rp[r1]);
+            out.vdest.push_back(0);
+            r = r1 - 1;
+            continue;
+        }
         if (len <= T) {
             out.vrow_ptr.push_back(rp[r + 1]);
             out.vdest.push_back((int32_t)r);
@@ -416,8 +481,14 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool
             out.nslots += pieces;
         }
     }
-    if (!any_split) out.vdest.clear();
-    pack_blocks(out.vrow_ptr, 0, (int64_t)out.vrow_ptr.size() - 1, cap, out, heavy_first);
+    if (!any_split && gaps.empty()) out.vdest.clear();
+    const int64_t nv = (int64_t)out.vrow_ptr.size() - 1;
+    int64_t v0 = 0;
+    for (int64_t gv : gaps) {
+        if (gv > v0) pack_blocks(out.vrow_ptr, v0, gv, cap, out, heavy_first);
+        v0 = gv + 1;
+    }
+    if (nv > v0) pack_blocks(out.vrow_ptr, v0, nv, cap, out, heavy_first);
 }
 
 // Every row's columns non-decreasing (coo_to_csr's output).  Column windows keep each row's CSR order only then.
@@ -681,6 +752,185 @@ int64_t window_cols(const spmm_hip_t *h, int kw, const std::vector<Piece> &pcs, 
     return (double)h->nnz >= WIN_MIN_SEG * (double)nseg ? W : 0;
 }
 
+// ---------------------------------------------------------------------------------------------- LDS B tiles
+// TILE mode (spmm_tile_kernel).  A tile is up to rmax consecutive rows of at most T nonzeros; its
+// REUSE is nnz / |union of its columns| -- how many times a B row staged in LDS is read.  The row kernel gathers
+// one B row per nonzero through L1/L2 (~15 TB/s chip-wide even at 92 % L2 hits); a tile stages each
+// B row of its union once and reads it from LDS.  Tiles whose reuse is below min_reuse stay with the row kernel
+// (the residual rows).  Chunks: the union is cut into pieces of <= uc columns and <= capa nonzeros.
+
+int tile_rpg(int g) { return std::max(1, std::min(8, TILE_RMAX / (WG / g))); }
+
+// Union columns a tile may hold (the kernel keeps them in LDS): the kernel's own constexpr for its template shape.
+template <typename T, int G>
+int tile_colmax_t() {
+    constexpr int NG = WG / G;
+    constexpr int RPG = NG * 8 <= TILE_RMAX ? 8 : (TILE_RMAX / NG > 1 ? TILE_RMAX / NG : 1);
+    return tile_colmax<T, 16 / (int)sizeof(T), G, TILE_UCB, TILE_CAPA, NG * RPG>();
+}
+int tile_colmax_for(size_t vsize, int g) {
+    auto pick = [&](auto t) -> int {
+        using T = decltype(t);
+        switch (g) {
+            case 4: return tile_colmax_t<T, 4>();
+            case 8: return tile_colmax_t<T, 8>();
+            case 16: return tile_colmax_t<T, 16>();
+            case 32: return tile_colmax_t<T, 32>();
+            default: return tile_colmax_t<T, 64>();
+        }
+    };
+    return vsize == 8 ? pick(0.0) : pick(0.0f);
+}
+
+struct TilePlan {
+    std::vector<int4> tiles;       // {first row, rows, first chunk, chunks}
+    std::vector<int4> chunks;      // {first tcol, columns, first nonzero (8-aligned), first tseg (8-aligned)} + sentinel
+    std::vector<int32_t> tcol;     // union columns, chunk by chunk
+    std::vector<uint16_t> tseg;    // per chunk: rows+1 segment offsets (relative to the chunk's first nonzero)
+    std::vector<int64_t> perm;     // chunk-major position -> original nonzero (-1: alignment padding)
+    std::vector<uint16_t> tlidx;   // chunk-major position -> chunk-local column
+    std::vector<uint8_t> in_tile;  // per row
+    int64_t rows = 0, nnz = 0;
+};
+
+// Reuse of rows [r0, r1): nnz / distinct columns (stamp/epoch marking; 0 for an empty range).  Stops counting once
+// the union makes the reuse fall below `floor` (returns what it has, which is then < floor).
+double tile_reuse(const int32_t *rp, const int32_t *col, int64_t r0, int64_t r1, std::vector<int32_t> &stamp,
+                  int32_t epoch, double floor, int64_t *nu_out) {
+    const int64_t nnz = (int64_t)rp[r1] - rp[r0];
+    int64_t nu = 0;
+    const int64_t nu_max = floor > 0 ? (int64_t)((double)nnz / floor) + 1 : INT64_MAX;
+    for (int64_t j = rp[r0]; j < rp[r1]; ++j) {
+        const int32_t c = col[j];
+        if (stamp[(size_t)c] != epoch) {
+            stamp[(size_t)c] = epoch;
+            if (++nu > nu_max) break;
+        }
+    }
+    if (nu_out) *nu_out = nu;
+    return nu > 0 ? (double)nnz / (double)nu : 0.0;
+}
+
+// Build the tiles.  A run of up to rmax consecutive rows of <= T nonzeros is a candidate; it becomes a tile when
+// its reuse is >= min_reuse, no column repeats more often than a chunk holds, its union fits the kernel's LDS column
+// list (<= colmax) and it makes <= dmax chunks -- a candidate over the last two is halved until it fits.  Rows must
+// be sorted (checked by the caller).  Returns false when no tile qualifies.
+bool build_tiles(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int rmax, int uc, int capa,
+                 double min_reuse, TilePlan &tp, int colmax = INT32_MAX, int dmax = INT32_MAX) {
+    tp = TilePlan();
+    tp.in_tile.assign((size_t)m, 0);
+    std::vector<int32_t> stamp((size_t)ncols, -1), pos((size_t)ncols, 0);
+    std::vector<int32_t> ulist, cnt;
+    int32_t epoch = 0;
+    auto next_epoch = [&]() {
+        if (epoch == INT32_MAX) {
+            std::fill(stamp.begin(), stamp.end(), -1);
+            epoch = 0;
+        }
+        return ++epoch;
+    };
+    auto eligible = [&](int64_t r) { return (int64_t)rp[r + 1] - rp[r] <= T; };
+    enum { TAKE, SKIP, SHRINK };
+    // evaluate (and on TAKE append) rows [r, r1)
+    auto attempt = [&](int64_t r, int64_t r1) -> int {
+        const int64_t nnz = (int64_t)rp[r1] - rp[r];
+        int64_t nu = 0;
+        const double reuse = tile_reuse(rp, col, r, r1, stamp, next_epoch(), min_reuse, &nu);
+        if (nnz == 0 || reuse < min_reuse) return SKIP;
+        // sorted union, local positions, per-column counts
+        ulist.clear();
+        const int32_t ep = next_epoch();
+        for (int64_t j = rp[r]; j < rp[r1]; ++j)
+            if (stamp[(size_t)col[j]] != ep) stamp[(size_t)col[j]] = ep, ulist.push_back(col[j]);
+        if ((int64_t)ulist.size() > colmax) return SHRINK;
+        std::sort(ulist.begin(), ulist.end());
+        cnt.assign(ulist.size(), 0);
+        for (size_t u = 0; u < ulist.size(); ++u) pos[(size_t)ulist[u]] = (int32_t)u;
+        const int nrows = (int)(r1 - r);
+        const int64_t room = capa - (int64_t)nrows * (TILE_SEG_ALIGN - 1);   // each row's padding (< 4 entries)
+        bool ok = room > 0;
+        for (int64_t j = rp[r]; j < rp[r1] && ok; ++j) ok = ++cnt[(size_t)pos[(size_t)col[j]]] <= room;
+        if (!ok) return nrows > 1 ? SHRINK : SKIP;
+        // chunk boundaries over the sorted union: <= uc columns and <= room entries
+        std::vector<size_t> cut{0};
+        for (size_t u0 = 0; u0 < ulist.size();) {
+            size_t u1 = u0;
+            int64_t cz = 0;
+            while (u1 < ulist.size() && (int64_t)(u1 - u0) < uc && (u1 == u0 || cz + cnt[u1] <= room)) cz += cnt[u1++];
+            cut.push_back(u1);
+            u0 = u1;
+        }
+        if ((int64_t)cut.size() - 1 > dmax) return SHRINK;
+        const int c_first = (int)tp.chunks.size();
+        std::vector<int32_t> rowp(rp + r, rp + r1);     // per row: next nonzero not yet placed
+        for (size_t ci = 0; ci + 1 < cut.size(); ++ci) {
+            const size_t u0 = cut[ci], u1 = cut[ci + 1];
+            int4 ch;
+            ch.x = (int)tp.tcol.size();
+            ch.y = (int)(u1 - u0);
+            ch.z = (int)tp.perm.size();
+            ch.w = (int)tp.tseg.size();
+            tp.tcol.insert(tp.tcol.end(), ulist.begin() + (ptrdiff_t)u0, ulist.begin() + (ptrdiff_t)u1);
+            int32_t off = 0;
+            for (int q = 0; q < nrows; ++q) {
+                tp.tseg.push_back((uint16_t)off);
+                int32_t &p = rowp[(size_t)q];
+                const int32_t pe = rp[r + q + 1];
+                while (p < pe && (size_t)pos[(size_t)col[p]] < u1) {
+                    tp.perm.push_back(p);
+                    tp.tlidx.push_back((uint16_t)(pos[(size_t)col[p]] - (int32_t)u0));
+                    ++p, ++off;
+                }
+                while (off % TILE_SEG_ALIGN) tp.perm.push_back(-1), tp.tlidx.push_back(TILE_PAD_LIDX), ++off;
+            }
+            tp.tseg.push_back((uint16_t)off);
+            while (tp.tseg.size() % 8) tp.tseg.push_back((uint16_t)off);
+            while (tp.perm.size() % 8) tp.perm.push_back(-1), tp.tlidx.push_back(0);
+            tp.chunks.push_back(ch);
+        }
+        tp.tiles.push_back(make_int4((int)r, nrows, c_first, (int)tp.chunks.size() - c_first));
+        for (int64_t q = r; q < r1; ++q) tp.in_tile[(size_t)q] = 1;
+        tp.rows += nrows;
+        tp.nnz += nnz;
+        return TAKE;
+    };
+    int64_t r = 0;
+    while (r < m) {
+        if (!eligible(r)) {
+            ++r;
+            continue;
+        }
+        int64_t r1 = r;
+        while (r1 < m && r1 - r < rmax && eligible(r1)) ++r1;
+        int st;
+        while ((st = attempt(r, r1)) == SHRINK && r1 - r > 1) r1 = r + (r1 - r) / 2;
+        r = r1;
+    }
+    tp.chunks.push_back(make_int4((int)tp.tcol.size(), 0, (int)tp.perm.size(), (int)tp.tseg.size()));
+    return !tp.tiles.empty();
+}
+
+// Policy gate: mean reuse over <= 256 evenly spaced candidate tiles (cheap; the full build only runs when tiles can
+// pay).  Returns the sampled mean reuse.
+double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int rmax) {
+    if (m == 0) return 0.0;
+    std::vector<int32_t> stamp((size_t)ncols, -1);
+    const int64_t ntiles = (m + rmax - 1) / rmax;
+    const int64_t ns = std::min<int64_t>(256, ntiles);
+    double sum = 0.0;
+    int64_t n = 0;
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t t = i * ntiles / ns;
+        const int64_t r0 = t * rmax, r1 = std::min<int64_t>(m, r0 + rmax);
+        bool ok = true;
+        for (int64_t r = r0; r < r1 && ok; ++r) ok = (int64_t)rp[r + 1] - rp[r] <= T;
+        if (!ok || rp[r1] == rp[r0]) continue;
+        sum += tile_reuse(rp, col, r0, r1, stamp, (int32_t)i, 0.0, nullptr);
+        ++n;
+    }
+    return n > 0 ? sum / (double)n : 0.0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -866,6 +1116,48 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     pl.seq_max = std::max(1, std::min(pl.seq_max, CAP));
     pl.cap = std::max(pl.cap, std::min(CAP, pow2_ceil(pl.seq_max)));   // a row of T nonzeros fits one block
 
+    // LDS B tiles: rows whose union of columns is reused enough leave the row kernel.  Needs 16-byte
+    // B pieces in every panel and sorted rows.  SPMM_HIP_TILES=-1 off / 1 every eligible tile; SPMM_HIP_TILE_REUSE
+    // sets the policy threshold.
+    TilePlan tp;
+    bool tiles = false;
+    const int64_t srow_t = (int64_t)pl.kw * (int64_t)h->vsize;
+    {
+        const int64_t srow = srow_t;
+        const int env_t = env_int("SPMM_HIP_TILES", 0);
+        const int forced = h->var.tiles != 0 ? h->var.tiles : env_t;
+        int vec_t, g_t;
+        lane_layout(pl.kw, k, h->vsize, vec_t, g_t);
+        const bool shape_ok = h->nnz > 0 && vec_t == (int)(16 / h->vsize) && ((int64_t)k * h->vsize) % 16 == 0 &&
+                              srow % 16 == 0 && k % pl.kw == 0 && srow >= 64 && srow <= 1024 &&
+                              pow2_ceil(srow / 16) == srow / 16 &&
+                              h->ncols < INT32_MAX;
+        const int64_t win_forced = h->var.win_bytes != 0 ? h->var.win_bytes : (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
+        if (forced >= 0 && shape_ok && win_forced <= 0) {
+            if (int st = load_cols()) return st;
+            if (rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
+                const int rows_env = env_int("SPMM_HIP_TILE_ROWS", 0);
+                int rmax = std::min((WG / g_t) * tile_rpg(g_t), rows_env > 0 ? rows_env : TILE_ROWS);
+                const char *thr = getenv("SPMM_HIP_TILE_REUSE");
+                const double min_reuse = forced > 0 ? 1.0 : (thr && *thr) ? atof(thr) : TILE_MIN_REUSE;
+                pl.tile_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax);
+                if (forced > 0 || pl.tile_reuse >= min_reuse)
+                    tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax,
+                                        (int)(TILE_UCB / srow), TILE_CAPA, min_reuse, tp,
+                                        tile_colmax_for(h->vsize, g_t) - 4, TILE_DMAX - 1);
+            }
+        }
+        if (tiles) {
+            pl.ntile = (int)tp.tiles.size();
+            pl.tile_rows = tp.rows;
+            pl.tile_nnz = tp.nnz;
+            pl.tile_chunks = (int64_t)tp.chunks.size() - 1;
+            // consecutive tiles share most of their columns: in XCD order they share an L2 as well
+            const int env_x = env_int("SPMM_HIP_TILE_XCD", 1);
+            pl.tile_xcd = (env_x > 0 && pl.ntile >= 64) ? 1 : 0;
+        }
+    }
+
     // XCD-contiguous order, else column windows (chained mode; needs every row's columns sorted); both decided from
     // col_idx on the host
     Inspection in;
@@ -881,7 +1173,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             if (int st = load_cols()) return st;
         }
         pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
-        if (maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
+        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
             std::vector<Piece> pcs;
             Inspection tmp;
             make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
@@ -895,7 +1187,8 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         pl.nwin = (int)in.win_blk.size() - 1;
         pl.nseg = (int64_t)in.vdest.size();
     } else {
-        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd);
+        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd,
+                tiles ? tp.in_tile.data() : nullptr);
         pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
     }
     h->nv = (int64_t)in.vrow_ptr.size() - 1;
@@ -1040,6 +1333,32 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         if (e == hipSuccess) e = alloc_copy((void **)&h->d_wcol, wcol.data(), wcol.size() * 4);
         if (e == hipSuccess) e = alloc_copy(&h->d_wval, wval.data(), wval.size());
         h->insp_bytes += wcol.size() * 4 + wval.size();
+    }
+    if (e == hipSuccess && tiles) {
+        // chunk-major copies of the tile rows' values and their chunk-local column indices (+ 64 B of padding)
+        std::vector<char> hval((size_t)h->nnz * h->vsize);
+        e = hipMemcpy(hval.data(), h->d_val, hval.size(), hipMemcpyDeviceToHost);
+        const size_t nz = tp.perm.size();
+        std::vector<char> tval(nz * h->vsize + PAD_BYTES, 0);
+        for (size_t q = 0; q < nz; ++q)
+            if (tp.perm[q] >= 0) std::memcpy(&tval[q * h->vsize], &hval[(size_t)tp.perm[q] * h->vsize], h->vsize);
+        // chunk-local column -> byte offset of its row in the staged B image (padding: the zero row after the image)
+        for (uint16_t &l : tp.tlidx) l = (l == TILE_PAD_LIDX) ? (uint16_t)TILE_UCB : (uint16_t)(l * srow_t);
+        tp.tlidx.resize(nz + PAD_BYTES / 2, 0);
+        tp.tseg.resize(tp.tseg.size() + PAD_BYTES / 2, 0);
+        tp.tcol.resize(tp.tcol.size() + PAD_BYTES / 4, 0);
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_tiles, tp.tiles.data(), tp.tiles.size() * sizeof(int4));
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_tchunk, tp.chunks.data(), tp.chunks.size() * sizeof(int4));
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_tcol, tp.tcol.data(), tp.tcol.size() * 4);
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_tseg, tp.tseg.data(), tp.tseg.size() * 2);
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_tlidx, tp.tlidx.data(), tp.tlidx.size() * 2);
+        if (e == hipSuccess) e = alloc_copy(&h->d_tval, tval.data(), tval.size());
+        if (e == hipSuccess && env_int("SPMM_HIP_TILE_STAMPS", 0)) {
+            e = hipMalloc((void **)&h->d_tstamps, tp.tiles.size() * 4 * sizeof(long long));
+            if (e == hipSuccess) e = hipMemset(h->d_tstamps, 0, tp.tiles.size() * 4 * sizeof(long long));
+        }
+        h->insp_bytes += tp.tiles.size() * sizeof(int4) + tp.chunks.size() * sizeof(int4) + tp.tcol.size() * 4 +
+                         tp.tseg.size() * 2 + tp.tlidx.size() * 2 + tval.size();
     }
     if (e != hipSuccess) {
         free_plan(h);
@@ -1192,7 +1511,28 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
     out[16] = h->plan.lmax;
     out[17] = h->plan.exact_rows;
     out[18] = h->fuse ? 1 : 0;
-    out[19] = 0;
+    out[19] = h->plan.ntile;
+    return SPMM_HIP_OK;
+}
+
+// Measurement only (SPMM_HIP_TILE_STAMPS=1 at plan time): per tile {start, end, wait, compute} s_memtime stamps of
+// the last tile launch.  Not in the public header.
+int spmm_hip_tile_stamps(spmm_hip_t *h, int64_t *out, int64_t n) {
+    if (!h || !out || !h->d_tstamps) return fail(SPMM_HIP_ERR_ARG, "tile_stamps: not enabled");
+    const int64_t cnt = std::min<int64_t>(n, (int64_t)h->plan.ntile * 4);
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, h->d_tstamps, (size_t)cnt * 8, hipMemcpyDeviceToHost));
+    return SPMM_HIP_OK;
+}
+
+int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out) {
+    if (!h || !out) return fail(SPMM_HIP_ERR_ARG, "tile_info: bad arguments");
+    out[0] = h->plan.ntile;
+    out[1] = h->plan.tile_rows;
+    out[2] = h->plan.tile_nnz;
+    out[3] = h->plan.tile_chunks;
+    out[4] = (int64_t)(h->plan.tile_reuse * 1000.0 + 0.5);
+    out[5] = h->plan.tile_xcd;
     return SPMM_HIP_OK;
 }
 
@@ -1258,6 +1598,51 @@ int spmm_hip_debug_inspect(const int32_t *row_ptr, const int32_t *col_idx, int64
     return SPMM_HIP_OK;
 }
 
+int spmm_hip_debug_tiles(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
+                         int32_t rmax, int32_t uc, int32_t capa, double min_reuse, int32_t colmax, int32_t dmax,
+                         spmm_hip_tiles_t *out) {
+    if (!row_ptr || !out || m < 0 || ncols < 0 || T < 1 || rmax < 1 || uc < 1 || capa < 1 || capa > 65535 ||
+        uc > 65536 || (!col_idx && m > 0 && row_ptr[m] > 0))
+        return fail(SPMM_HIP_ERR_ARG, "debug_tiles: bad arguments");
+    std::memset(out, 0, sizeof(*out));
+    if (!rows_sorted(row_ptr, col_idx, m)) return fail(SPMM_HIP_ERR_CSR, "debug_tiles: unsorted row");
+    TilePlan tp;
+    build_tiles(row_ptr, col_idx, m, ncols, T, rmax, uc, capa, min_reuse, tp, colmax > 0 ? colmax : INT32_MAX,
+                dmax > 0 ? dmax : INT32_MAX);
+    auto dup = [](const auto &v) {
+        using E = typename std::decay_t<decltype(v)>::value_type;
+        E *p = (E *)malloc(std::max<size_t>(v.size(), 1) * sizeof(E));
+        if (p && !v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(E));
+        return p;
+    };
+    out->ntile = (int64_t)tp.tiles.size();
+    out->nchunk = (int64_t)tp.chunks.size() - 1;
+    out->ncol = (int64_t)tp.tcol.size();
+    out->nseg = (int64_t)tp.tseg.size();
+    out->nz = (int64_t)tp.perm.size();
+    out->m = m;
+    out->tiles = (int32_t *)dup(tp.tiles);
+    out->chunks = (int32_t *)dup(tp.chunks);
+    out->tcol = dup(tp.tcol);
+    out->tseg = dup(tp.tseg);
+    out->tlidx = dup(tp.tlidx);
+    out->perm = dup(tp.perm);
+    out->in_tile = dup(tp.in_tile);
+    return SPMM_HIP_OK;
+}
+
+void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t) {
+    if (!t) return;
+    free(t->tiles);
+    free(t->chunks);
+    free(t->tcol);
+    free(t->tseg);
+    free(t->tlidx);
+    free(t->perm);
+    free(t->in_tile);
+    std::memset(t, 0, sizeof(*t));
+}
+
 void spmm_hip_debug_free(spmm_hip_inspection_t *ins) {
     if (!ins) return;
     free(ins->vrow_ptr);
@@ -1285,6 +1670,7 @@ int spmm_hip_tune_select(spmm_hip_t *h, int u, int ntc, int dma, int buf, int se
     h->var.win_bytes = win_bytes;
     h->var.xcd = xcd;
     h->var.lanes = lanes;
+    h->var.tiles = env_int("SPMM_HIP_TUNE_TILES", 0);
     const int k = h->plan.k;
     h->plan.k = -1;
     return k > 0 ? spmm_hip_plan(h, k) : SPMM_HIP_OK;

@@ -423,6 +423,207 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
     }
 }
 
+// ------------------------------------------------------------------------------------------------ LDS B tiles
+// TILE mode: for rows that share their columns -- similar consecutive rows (cross-row similarity) or
+// dense column bands -- the row kernel re-gathers the same B row once per nonzero through L1/L2 (~15 TB/s chip-wide,
+// the TA/L2 request path), while the LDS reads at ~150 TB/s.  A TILE is up to RMAX consecutive C rows; the
+// inspector lists the union U of their columns (sorted) and cuts it into CHUNKS of <= UCB bytes of B rows and <=
+// CAPA entries.  Per chunk the workgroup stages (LDS-DMA) the chunk's B rows and the chunk's entries from a
+// chunk-major copy of A: values and 16-bit byte offsets of their B rows in the staged image, row by row, each
+// row's segment padded to a multiple of 4 entries with (value +0, the all-zero B row) -- fma(+0, +0, acc) == acc
+// exactly because a chain that starts from +0 can never hold -0 -- so the inner loop reads 4 offsets and 4 values
+// per step with no predication.  Row group g (G lanes, VEC columns each) owns rows g, g+NG, ... of the tile and
+// carries their accumulators in registers across chunks; chunks go in column order and each row's columns are
+// sorted, so every row is still ONE fused multiply-add chain from 0 in CSR order -- bit-identical to the
+// reference, like an unsplit row of the row kernel.  Descriptors:
+//   tiles[t]  = {first C row, rows, first chunk, chunks}
+//   tchunk[c] = {first union column (tcol), columns, first entry (tval/toff, 8-aligned), first segment offset
+//               (tseg, 8-aligned)}; chunk c's staged sizes are the gaps to chunk c+1 (a sentinel ends the table)
+//   tseg[...] = per chunk, rows+1 entry offsets (relative to the chunk's first entry; multiples of 4)
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+// LDS budget of one tile workgroup (3 per CU: 3 x 53,248 B with the 512-B allocation granule).
+constexpr int TILE_LDS_BYTES = 53248;
+constexpr int TILE_DMAX = 64;                  // chunk descriptors per tile (incl. the end marker)
+
+template <typename T, int VEC, int G, int UCB, int CAPA, int RMAX>
+struct TileBuf {
+    vec<T, VEC> b[UCB / 16 + G];                  // staged B rows, then the zero row (byte offset UCB)
+    vec<T, 4> v[CAPA / 4];                        // the chunk's values, 4 per step
+    u16x4 o[CAPA / 4];                            // byte offset (in b) of each value's B row, 4 per step
+    uint16_t s[RMAX + 8];                         // row segment offsets (entries)
+};
+// Union columns one tile may hold in LDS (the rest of the budget after two chunk buffers and the descriptors).
+template <typename T, int VEC, int G, int UCB, int CAPA, int RMAX>
+constexpr int tile_colmax() {
+    return (int)((TILE_LDS_BYTES - 2 * (int)sizeof(TileBuf<T, VEC, G, UCB, CAPA, RMAX>) - TILE_DMAX * 16) / 4) & ~63;
+}
+
+// One row segment [a4, e4) (in steps of 4 entries), two steps per iteration: the offsets and values of both steps
+// are read together, then the 8 B rows, so each pair of steps waits on two LDS round trips (offsets, B rows).
+// `bl` = the lane's byte address in the B image.
+template <typename T, int VEC, typename Buf>
+__device__ __forceinline__ void tile_step(vec<T, VEC> &acc, const char *bb, int bl, const u16x4 o,
+                                          const vec<T, 4> &av) {
+    using V = vec<T, VEC>;
+    const V b0 = *reinterpret_cast<const V *>(bb + (bl + (int)o.x));
+    const V b1 = *reinterpret_cast<const V *>(bb + (bl + (int)o.y));
+    const V b2 = *reinterpret_cast<const V *>(bb + (bl + (int)o.z));
+    const V b3 = *reinterpret_cast<const V *>(bb + (bl + (int)o.w));
+    vfma(acc, av.v[0], b0);
+    vfma(acc, av.v[1], b1);
+    vfma(acc, av.v[2], b2);
+    vfma(acc, av.v[3], b3);
+}
+
+template <typename T, int VEC, typename Buf>
+__device__ __forceinline__ vec<T, VEC> tile_dot(vec<T, VEC> acc, const Buf &cur, int bl, int a4, int e4) {
+    using V = vec<T, VEC>;
+    const char *bb = reinterpret_cast<const char *>(cur.b);
+    int t = a4;
+    for (; t + 2 <= e4; t += 2) {
+        const u16x4 o0 = cur.o[t], o1 = cur.o[t + 1];
+        const vec<T, 4> v0 = cur.v[t], v1 = cur.v[t + 1];
+        const V b0 = *reinterpret_cast<const V *>(bb + (bl + (int)o0.x));
+        const V b1 = *reinterpret_cast<const V *>(bb + (bl + (int)o0.y));
+        const V b2 = *reinterpret_cast<const V *>(bb + (bl + (int)o0.z));
+        const V b3 = *reinterpret_cast<const V *>(bb + (bl + (int)o0.w));
+        const V b4 = *reinterpret_cast<const V *>(bb + (bl + (int)o1.x));
+        const V b5 = *reinterpret_cast<const V *>(bb + (bl + (int)o1.y));
+        const V b6 = *reinterpret_cast<const V *>(bb + (bl + (int)o1.z));
+        const V b7 = *reinterpret_cast<const V *>(bb + (bl + (int)o1.w));
+        vfma(acc, v0.v[0], b0);
+        vfma(acc, v0.v[1], b1);
+        vfma(acc, v0.v[2], b2);
+        vfma(acc, v0.v[3], b3);
+        vfma(acc, v1.v[0], b4);
+        vfma(acc, v1.v[1], b5);
+        vfma(acc, v1.v[2], b6);
+        vfma(acc, v1.v[3], b7);
+    }
+    if (t < e4) tile_step<T, VEC, Buf>(acc, bb, bl, cur.o[t], cur.v[t]);
+    return acc;
+}
+
+// LDS-DMA of `bytes` (multiple of 16) from src to the LDS at dst by the whole workgroup, 1-KiB wave pieces.
+__device__ __forceinline__ void dma_to_lds(const char *src, char *dst, int bytes, int wave, int wl) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    for (int q = wave; q * 1024 < bytes; q += WG / 64) {
+        const int off = q * 1024 + wl * 16;
+        if (off < bytes) __builtin_amdgcn_global_load_lds((const void *)(src + off), (lds_void *)(dst + q * 1024), 16, 0, 0);
+    }
+}
+
+// Prologue: the tile's chunk descriptors and its whole union of columns land in LDS by one DMA round trip, so the
+// chunk loop never waits on a global or scalar load.  Chunk pipeline (double-buffered LDS): at the top of step c
+// the workgroup waits for chunk c's DMA (issued one step earlier) and passes a barrier (so every wave is done with
+// the buffer chunk c+1 will fill), issues chunk c+1's DMA (B rows from the LDS column list), then computes chunk c
+// while c+1 lands.
+template <typename T, int VEC, int G, int RPG, int UCB, int CAPA, bool NTC, bool XCD>
+__global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict__ tiles,
+                                                          const int4 *__restrict__ tchunk,
+                                                          const int32_t *__restrict__ tcol,
+                                                          const uint16_t *__restrict__ tseg,
+                                                          const T *__restrict__ tval,
+                                                          const uint16_t *__restrict__ toff,
+                                                          const T *__restrict__ B, T *__restrict__ C, int ld,
+                                                          long long *__restrict__ stamps) {
+    constexpr int NG = WG / G;
+    constexpr int RMAX = NG * RPG;
+    constexpr int NPL = UCB / 16 / WG;             // B pieces per lane per chunk
+    constexpr int LPPR = __builtin_ctz(G);         // 16-byte pieces per staged B row == G (power of two, host)
+    static_assert(UCB % (16 * WG) == 0, "UCB must be a multiple of 4 KiB");
+    static_assert(VEC * sizeof(T) == 16, "16-byte lanes");
+    using V = vec<T, VEC>;
+    using Buf = TileBuf<T, VEC, G, UCB, CAPA, RMAX>;
+    constexpr int COLMAX = tile_colmax<T, VEC, G, UCB, CAPA, RMAX>();
+    // two DISTINCT LDS objects (not an array): the compiler can then tell the chunk being read from the one the DMA
+    // is filling and does not insert a vmcnt(0) wait in front of the compute's LDS reads
+    __shared__ __attribute__((aligned(16))) Buf sbuf0;
+    __shared__ __attribute__((aligned(16))) Buf sbuf1;
+    __shared__ __attribute__((aligned(16))) int4 sdesc[TILE_DMAX];
+    __shared__ __attribute__((aligned(16))) int32_t scol[COLMAX];
+    typedef __attribute__((address_space(3))) void lds_void;
+
+    const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int4 tl = tiles[b];
+    const int tid = threadIdx.x, wave = tid / 64, wl = tid % 64;
+    const int grp = tid / G, lane = tid % G;
+    if (tid < G) {
+        sbuf0.b[UCB / 16 + tid] = vzero<T, VEC>();
+        sbuf1.b[UCB / 16 + tid] = vzero<T, VEC>();
+    }
+    V acc[RPG];
+#pragma unroll
+    for (int q = 0; q < RPG; ++q) acc[q] = vzero<T, VEC>();
+    const long long t_start = stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+
+    // prologue: descriptors [tl.z, tl.z + tl.w] (the last one is the next chunk: sizes) and the union columns
+    const int col0 = tchunk[tl.z].x, col1 = tchunk[tl.z + tl.w].x;
+    dma_to_lds((const char *)(tchunk + tl.z), (char *)sdesc, (tl.w + 1) * 16, wave, wl);
+    {   // tcol is 64-B padded on the device; copy from the 16-B boundary below col0
+        const int c0a = col0 & ~3;
+        dma_to_lds((const char *)(tcol + c0a), (char *)scol, ((col1 - c0a + 3) & ~3) * 4, wave, wl);
+    }
+    const int cbase = col0 & ~3;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const char *Bb = reinterpret_cast<const char *>(B);
+    const size_t ldb = (size_t)ld * sizeof(T);
+    auto issue = [&](int c, Buf &bf) {
+        const int4 ch = sdesc[c], cn = sdesc[c + 1];
+        dma_to_lds((const char *)(tval + ch.z), (char *)bf.v, (cn.z - ch.z) * (int)sizeof(T), wave, wl);
+        dma_to_lds((const char *)(toff + ch.z), (char *)bf.o, (cn.z - ch.z) * 2, wave, wl);
+        dma_to_lds((const char *)(tseg + ch.w), (char *)bf.s, (cn.w - ch.w) * 2, wave, wl);
+        const int np = ch.y << LPPR;
+#pragma unroll
+        for (int it = 0; it < NPL; ++it) {
+            const int p = it * WG + tid;
+            if (p < np) {
+                const int row = scol[ch.x - cbase + (p >> LPPR)];
+                const char *g = Bb + (size_t)row * ldb + (p & (G - 1)) * 16;
+                __builtin_amdgcn_global_load_lds((const void *)g, (lds_void *)(bf.b + it * WG + wave * 64), 16, 0, 0);
+            }
+        }
+    };
+    long long t_wait = 0, t_comp = 0, t_mark = 0;        // measurement only (stamps != nullptr)
+    auto step = [&](const Buf &cur, Buf &nxt, int c) {
+        if (stamps) t_mark = (long long)__builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk c landed
+        __syncthreads();                                     // ... for every wave; chunk c-1's buffer is free
+        if (stamps) {
+            const long long t = (long long)__builtin_amdgcn_s_memtime();
+            t_wait += t - t_mark;
+            t_mark = t;
+        }
+        if (c + 1 < tl.w) issue(c + 1, nxt);
+#pragma unroll
+        for (int q = 0; q < RPG; ++q) {
+            const int r = grp + q * NG;
+            if (r < tl.y) acc[q] = tile_dot<T, VEC>(acc[q], cur, lane * 16, cur.s[r] >> 2, cur.s[r + 1] >> 2);
+        }
+        if (stamps) t_comp += (long long)__builtin_amdgcn_s_memtime() - t_mark;
+    };
+    issue(0, sbuf0);
+    for (int c = 0; c < tl.w; c += 2) {
+        step(sbuf0, sbuf1, c);
+        if (c + 1 < tl.w) step(sbuf1, sbuf0, c + 1);
+    }
+#pragma unroll
+    for (int q = 0; q < RPG; ++q) {
+        const int r = grp + q * NG;
+        if (r < tl.y) vstore<T, VEC, NTC>(C + (size_t)(tl.x + r) * ld + lane * VEC, acc[q]);
+    }
+    if (stamps && tid == 0) {
+        long long *st = stamps + (size_t)b * 4;
+        st[0] = t_start;
+        st[1] = (long long)__builtin_amdgcn_s_memtime();
+        st[2] = t_wait;
+        st[3] = t_comp;
+    }
+}
+
 // long_rows[b] = {row, first_slot, nslots, 0}: C[row][n] = sum of the row's partial slots P[first_slot + q][n].
 // Separate combine launch (column-window plans, or partials beyond 4 GiB): one workgroup per split row.
 template <typename T>

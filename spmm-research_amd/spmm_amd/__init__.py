@@ -93,6 +93,13 @@ class _Inspection(C.Structure):
                 ("perm", C.POINTER(C.c_int64))]
 
 
+class _Tiles(C.Structure):
+    _fields_ = [("ntile", _i64), ("nchunk", _i64), ("ncol", _i64), ("nseg", _i64), ("nz", _i64), ("m", _i64),
+                ("tiles", C.POINTER(C.c_int32)), ("chunks", C.POINTER(C.c_int32)), ("tcol", C.POINTER(C.c_int32)),
+                ("tseg", C.POINTER(C.c_uint16)), ("tlidx", C.POINTER(C.c_uint16)), ("perm", C.POINTER(C.c_int64)),
+                ("in_tile", C.POINTER(C.c_uint8))]
+
+
 def _bind_hip(L: C.CDLL) -> C.CDLL:
     vp, i32, i64 = C.c_void_p, C.c_int32, _i64
     L.spmm_hip_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)]
@@ -113,6 +120,11 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_debug_inspect.argtypes = [_i32p, _i32p, i64, i64, i32, i32, i64, C.POINTER(_Inspection)]
     L.spmm_hip_debug_free.argtypes = [C.POINTER(_Inspection)]
     L.spmm_hip_debug_free.restype = None
+    L.spmm_hip_tile_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
+    L.spmm_hip_debug_tiles.argtypes = [_i32p, _i32p, i64, i64, i32, i32, i32, i32, C.c_double, i32, i32,
+                                       C.POINTER(_Tiles)]
+    L.spmm_hip_debug_tiles_free.argtypes = [C.POINTER(_Tiles)]
+    L.spmm_hip_debug_tiles_free.restype = None
     L.spmm_hip_strerror.argtypes = [C.c_int]
     L.spmm_hip_strerror.restype = C.c_char_p
     L.spmm_hip_last_error_detail.restype = C.c_char_p
@@ -318,6 +330,26 @@ def debug_inspect(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, T: int, 
     return out
 
 
+def debug_tiles(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, T: int, rmax: int = 64, uc: int = 128,
+                capa: int = 2048, min_reuse: float = 4.0, colmax: int = 0, dmax: int = 0) -> dict:
+    """The tile decomposition (host only; spmm_hip_debug_tiles): tiles, chunks, union columns, per-chunk segment
+    offsets, the chunk-major nonzero permutation (-1 = padding), chunk-local columns and the rows in tiles."""
+    rp = np.ascontiguousarray(row_ptr, np.int32)
+    ci = np.ascontiguousarray(col_idx if len(col_idx) else np.zeros(1), np.int32)
+    t = _Tiles()
+    _check("debug_tiles", hip.spmm_hip_debug_tiles(rp, ci, len(rp) - 1, ncols, T, rmax, uc, capa, min_reuse,
+                                                   colmax, dmax, C.byref(t)))
+    try:
+        def arr(p, n):
+            return np.ctypeslib.as_array(p, (max(n, 1),))[:n].copy()
+        out = {"tiles": arr(t.tiles, 4 * t.ntile).reshape(-1, 4), "chunks": arr(t.chunks, 4 * (t.nchunk + 1)).reshape(-1, 4),
+               "tcol": arr(t.tcol, t.ncol), "tseg": arr(t.tseg, t.nseg), "tlidx": arr(t.tlidx, t.nz),
+               "perm": arr(t.perm, t.nz), "in_tile": arr(t.in_tile, t.m).astype(bool)}
+    finally:
+        hip.spmm_hip_debug_tiles_free(C.byref(t))
+    return out
+
+
 def device_count() -> int:
     n = C.c_int()
     hip.spmm_hip_device_count(C.byref(n))
@@ -379,6 +411,13 @@ class MatrixFormat:
         out = np.zeros(INFO_SLOTS, np.int64)
         _check("info", hip.spmm_hip_info(self._h, out))
         return out
+
+    def tile_info(self) -> dict:
+        """LDS B tiles of the current plan (spmm_hip_tile_info)."""
+        out = np.zeros(6, np.int64)
+        _check("tile_info", hip.spmm_hip_tile_info(self._h, out))
+        return {"tiles": int(out[0]), "rows": int(out[1]), "nnz": int(out[2]), "chunks": int(out[3]),
+                "reuse": out[4] / 1000.0, "xcd": int(out[5])}
 
     def exact_rows(self) -> np.ndarray:
         """bool[m]: rows computed as the reference's single left-to-right FMA chain (bit-identical to it)."""
