@@ -16,6 +16,10 @@ Workloads (--workload):
             gamma row lengths: 7477550 7477550 20 6.6667 gamma random 0.3 10000 0.95 0.5 14 (150 M nonzeros).
   medium-sample  (config 3) every --sample-stride-th line of synthetic_matrices_medium_dataset (N=1 only); value =
             aggregate GFLOP/s over the sample (sum of flops / sum of kernel time).
+  pipeline   the sparse-attention pipeline consumer, fp32, n=512: K/Q/V = W x (DLMC-like 512 x 512
+            attention weights, 70 % pruned), SDDMM over a band+random mask (band 16, 5 % dense), final SpMM;
+            one step = the reference compute() step (pipeline_code_bench/sddmm_bench.cpp:918-937), HBM-resident,
+            captured in a hipGraph; GFLOP/s by the reference formula (:978-983).  N=1 only.
 A values: the generator's seeded U[0.5, 1.5).  B: drand48(seed 42), drawn on the host in the reference harness's
 column-major layout [K][ncols] (the same x the CPU baseline multiplies), uploaded transposed to the engine's
 row-major layout, resident in HBM.
@@ -52,6 +56,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
+# the CPUs this process may use, read before the HIP runtime starts: on the GPU box the runtime narrows the main
+# thread's affinity (2 of 256 CPUs were seen), which OpenMP threads started later would inherit
+_AFFINITY0 = os.sched_getaffinity(0)
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "GFLOP/s + achieved HBM GB/s, synthetic medium dataset, CSR SpMM K=32 fp64"
@@ -64,7 +71,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
-    ap.add_argument("--workload", choices=["config2", "config4", "medium-sample"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config4", "medium-sample", "pipeline"], default="config2")
+    ap.add_argument("--pipe-m", type=int, default=512, help="pipeline: weight rows = mask size")
+    ap.add_argument("--pipe-k", type=int, default=512, help="pipeline: weight columns (rows of x)")
+    ap.add_argument("--pipe-n", type=int, default=512, help="pipeline: columns of x (NUM_COLS)")
+    ap.add_argument("--pipe-density", type=float, default=0.3, help="pipeline: weight density (1 - pruning)")
+    ap.add_argument("--pipe-mask-density", type=float, default=0.05)
+    ap.add_argument("--pipe-band", type=int, default=16)
+    ap.add_argument("--pipe-mode", type=int, default=0, help="pipeline: SDDMM flags (0 reference, 1 QK^T, |2 softmax)")
     ap.add_argument("--gen", default=None, help="override: 11-field generator line of the global matrix")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--sample-stride", type=int, default=160, help="medium-sample: every n-th dataset line")
@@ -90,9 +104,21 @@ def spawn_ranks(n: int) -> int:
 
 
 def cpu_share() -> tuple[int, str]:
-    """Threads for the CPU baseline: the CPUs this process may run on, capped by OMP_NUM_THREADS when the
-    environment sets it (the GPU box sets it to its per-GPU CPU share, 16); and the CPU model."""
-    n = len(os.sched_getaffinity(0))
+    """Threads for the CPU baseline: the CPUs this process may run on (its affinity at start; restored here for
+    this thread, so the OpenMP team the baseline starts can use them), capped by the cgroup CPU quota and by
+    OMP_NUM_THREADS when the environment sets it (the GPU box: quota 16 CPUs, OMP_NUM_THREADS=16); and the CPU
+    model."""
+    try:
+        os.sched_setaffinity(0, _AFFINITY0)
+    except OSError:
+        pass
+    n = len(_AFFINITY0)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
     omp = os.environ.get("OMP_NUM_THREADS", "")
     if omp.isdigit() and int(omp) > 0:
         n = min(n, int(omp))
@@ -133,10 +159,16 @@ def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
 
     def call():
         fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, x, y, k, threads)
+    # the reference harness's 100 warm-ups (spmv_bench.cpp:316-320), bounded to ~15 s of CPU time so the default
+    # bench finishes in minutes on a box that gives the process few cores
     t0 = time.perf_counter()
-    for _ in range(warmup):
+    call()
+    t_first = time.perf_counter() - t0
+    warmup = max(1, min(warmup, int(15.0 / max(t_first, 1e-6))))
+    t0 = time.perf_counter()
+    for _ in range(warmup - 1):
         call()
-    t_warm = time.perf_counter() - t0
+    t_warm = time.perf_counter() - t0 + t_first
     times = []
     t_end = time.perf_counter() + budget_s
     while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 100):
@@ -242,6 +274,89 @@ def run_medium_sample(args, torch, S, np):
     return 0 if bad == 0 else 1
 
 
+def run_pipeline(args, torch, S, np):
+    """one reference compute() step on the engine, graph-captured, fp32 by default."""
+    from spmm_amd import pipeline as P
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    npdt = np.float64 if args.dtype == "f64" else np.float32
+    tdt = torch.float64 if args.dtype == "f64" else torch.float32
+    m, k, n = args.pipe_m, args.pipe_k, args.pipe_n
+    w = [P.dlmc_like_weight(m, k, args.pipe_density, 100 + i) for i in range(3)]
+    mask = P.band_and_random_mask(m, args.pipe_mask_density, args.pipe_band, 107)
+    x = S.drand48(42, k * n).reshape(k, n)
+    pipe = P.SparseAttentionPipeline(*w, mask, n, npdt, args.pipe_mode)
+    bx = torch.from_numpy(x.astype(npdt)).to(dev)
+    bufs = [torch.zeros((m, n), dtype=tdt, device=dev) for _ in range(3)]
+    y = torch.zeros(mask.nnz, dtype=tdt, device=dev)
+    out = torch.zeros((m, n), dtype=tdt, device=dev)
+    s = torch.cuda.Stream(dev)
+    ptrs = (bx.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr(), y.data_ptr(), out.data_ptr())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            pipe.run_device(*ptrs, s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        pipe.run_device(*ptrs, s.cuda_stream)
+    for _ in range(args.warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(s)
+    with torch.cuda.stream(s):
+        for _ in range(args.steps):
+            g.replay()
+    ev1.record(s)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    step_ms = ev0.elapsed_time(ev1) / args.steps
+    # parity of this run, stage by stage against the oracle on the GPU's own stage inputs (test infrastructure
+    # as the checker): SDDMM bit-exact; K/Q/V on the rows the engine reports exact
+    ok = True
+    for t, a, b in zip("KQV", w, bufs):
+        ex = pipe.mf[t].exact_rows()
+        want = O.spmm_rowmajor(a.row_ptr, a.col_idx, a.values.astype(npdt), k, x.astype(npdt))
+        ok = ok and np.array_equal(b.cpu().numpy()[ex], want[ex])
+    if not args.pipe_mode & 2:
+        yo = O.sddmm(mask.row_ptr, mask.col_idx, mask.values.astype(npdt), bufs[1].cpu().numpy(),
+                     bufs[0].cpu().numpy(), args.pipe_mode & 1)
+        ok = ok and np.array_equal(y.cpu().numpy(), yo)
+    flops = pipe.flops
+    # CPU baseline: the oracle's stages (the reference compute() step's arithmetic) on this host, bounded sample
+    cpu = None
+    if not args.no_cpu_baseline:
+        threads, model = cpu_share()
+        ts = []
+        t_end = time.perf_counter() + args.cpu_seconds
+        while len(ts) < 3 or (time.perf_counter() < t_end and len(ts) < 50):
+            t1 = time.perf_counter()
+            Kc, Qc, Vc = (O.spmm_rowmajor(a.row_ptr, a.col_idx, a.values.astype(npdt), k, x.astype(npdt)) for a in w)
+            yc = O.sddmm(mask.row_ptr, mask.col_idx, mask.values.astype(npdt), Qc, Kc, args.pipe_mode & 1)
+            O.spmm_rowmajor(mask.row_ptr, mask.col_idx, yc, m, Vc)
+            ts.append(time.perf_counter() - t1)
+        ts.sort()
+        cpu = {"value": round(flops / ts[len(ts) // 2] / 1e9, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+               "sample": f"one pipeline step per call, oracle C restatement (SpMMs {threads} OpenMP threads, SDDMM "
+                         f"serial) on {model}; {len(ts)} calls, median {ts[len(ts) // 2] * 1e3:.2f} ms"}
+    line = {
+        "metric": "GFLOP/s, sparse-attention pipeline step (SpMM K,Q,V + SDDMM + SpMM), reference formula",
+        "value": round(flops / (step_ms * 1e-3) / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_ms, 5), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (DLMC-like random-pruned weights U[-1,1), seeded band+random mask, x drand48(42))",
+        "config": {"workload": f"pipeline: m={m} k={k} n={n} weight density {args.pipe_density} mask density "
+                               f"{args.pipe_mask_density} band {args.pipe_band} sddmm flags {args.pipe_mode}",
+                   "nnz": [a.nnz for a in w] + [mask.nnz], "parallelism": "single-gpu"},
+        "wall_ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "cpu_baseline": cpu, "setup": {"stages_bitexact_vs_oracle": ok},
+    }
+    print(json.dumps(line), flush=True)
+    pipe.close()
+    return 0 if ok else 1
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -267,6 +382,14 @@ def main():
     if not torch.cuda.is_available():
         print("error: no HIP device visible (bench.py measures the GPU engine; there is no CPU path)", file=sys.stderr)
         sys.exit(3)
+    if args.workload == "pipeline":
+        if N != 1:
+            print("error: --workload pipeline runs on one GPU", file=sys.stderr)
+            sys.exit(2)
+        torch.cuda.set_device(0)
+        if args.dtype == "f64" and "--dtype" not in sys.argv:
+            args.dtype = "f32"                       # the reference pipeline's configuration
+        sys.exit(run_pipeline(args, torch, S, np))
     if args.workload == "medium-sample":
         if N != 1:
             print("error: --workload medium-sample runs on one GPU", file=sys.stderr)

@@ -81,6 +81,17 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
  * spmm_hip_run (SPMM_HIP_ASSUME_X_UNCHANGED). */
 int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *d_c, int32_t k, void *stream);
 
+/* Execute, host buffers with B ROW-major (x[col*k + n]; the layout the reference pipeline plugin hands MKL's csrmm,
+ * pipeline_code_bench/sddmm_taco_naive.cpp:219-249): uploads x into the engine's B directly (no transpose), runs,
+ * downloads y (row-major [m][k]).  Synchronous. */
+int spmm_hip_run_rowmajor(spmm_hip_t *h, const void *x, void *y, int32_t k);
+
+/* Replace A's values (same pattern): host array (synchronous) or device array (stream-ordered, graph-capturable).
+ * The sparse-attention pipeline's final SpMM multiplies by the SDDMM output, which changes every run
+ * (pipeline_code_bench/sddmm_bench.cpp:934-936).  Window-major / tile copies of the values are re-gathered. */
+int spmm_hip_update_values(spmm_hip_t *h, const void *vals);
+int spmm_hip_update_values_device(spmm_hip_t *h, const void *d_vals, void *stream);
+
 /* Plan for k without running: the inspector (lane layout, block capacity, split length T, K panels of 256-byte B
  * rows when B would crowd the Infinity Cache -- SPMM_HIP_PANEL_K=<cols> overrides) and all allocations happen here, not in
  * run_device. */

@@ -51,6 +51,10 @@ def lib() -> C.CDLL:
         L.oracle_check_accuracy.argtypes = [C.c_void_p, _f64p, i64, C.c_double, _f64p]
         L.oracle_coo_to_csr.argtypes = [_i32p, _i32p, C.c_void_p, i64, i64, _i32p, _i32p, _f64p]
         L.oracle_drand48_fill.argtypes = [i64, _f64p, i64]
+        L.oracle_sddmm_d.argtypes = [_i32p, _i32p, _f64p, i64, _f64p, _f64p, C.c_int32, C.c_int32, _f64p]
+        L.oracle_sddmm_f.argtypes = [_i32p, _i32p, _f32p, i64, _f32p, _f32p, C.c_int32, C.c_int32, _f32p]
+        L.oracle_softmax_d.argtypes = [_f64p, i64]
+        L.oracle_softmax_f.argtypes = [_f32p, i64]
         _oracle = L
     return _oracle
 
@@ -204,3 +208,34 @@ def ref_metrics(gold_d, test_d) -> np.ndarray:
     t = np.ascontiguousarray(test_d, np.float64).ravel()
     ref_lib("d").ref_metrics(g, t, len(g), out)
     return out
+
+
+# ---------------------------------------------------------------------------------------- sparse-attention pipeline
+def sddmm(row_ptr, col_idx, mask_vals, Q, K, mode: int = 0) -> np.ndarray:
+    """Pipeline SDDMM (sddmm_taco_naive.cpp:98-140): mode 0 = the reference's row-i-of-K product, 1 = Q K^T."""
+    L = lib()
+    dt = np.asarray(mask_vals).dtype
+    m = len(row_ptr) - 1
+    Q = np.ascontiguousarray(Q, dt)
+    K = np.ascontiguousarray(K, dt)
+    n = Q.shape[1]
+    y = np.zeros(int(row_ptr[-1]), dt)
+    fn = L.oracle_sddmm_d if dt == np.float64 else L.oracle_sddmm_f
+    fn(np.ascontiguousarray(row_ptr, np.int32), np.ascontiguousarray(col_idx, np.int32),
+       np.ascontiguousarray(mask_vals, dt), m, Q.ravel(), K.ravel(), n, mode, y)
+    return y
+
+
+def softmax(y: np.ndarray) -> np.ndarray:
+    """The reference softmax over all nonzeros (sddmm_taco_naive.cpp:191-209), serial."""
+    y = np.array(y, copy=True)
+    (lib().oracle_softmax_d if y.dtype == np.float64 else lib().oracle_softmax_f)(y, len(y))
+    return y
+
+
+def spmm_rowmajor(row_ptr, col_idx, vals, ncols: int, x_rowmajor: np.ndarray) -> np.ndarray:
+    """compute_csr's chain (spmm_kernel_csr.cpp:70-96) with B given row-major [ncols][n] (the pipeline's MKL
+    layout): the same per-entry fma chain, the column-major view is just a transpose."""
+    x = np.asarray(x_rowmajor)
+    n = x.shape[1]
+    return spmm(row_ptr, col_idx, vals, ncols, np.ascontiguousarray(x.T).ravel(), n)

@@ -19,6 +19,12 @@
  *                             lib/array_metrics.c:1472 mae, :1528 max_ae, :1586 mse, :1643/1696 mape,
  *                             :1754/1810 smape, :1925 lnQ, :1996 mlare, :2112 gmare)
  *   oracle_coo_to_csr         lib/storage_formats/csr/csr_gen.c:163-217 (bucket by row, scatter, sort columns)
+ *   oracle_sddmm_{d,f}        benchmark_code/CPU/AMD/pipeline_code_bench/sddmm_taco_naive.cpp:98-140 (compute2) and
+ *                             :280-290 (compute_csr zeroes y first): the sparse-attention pipeline's SDDMM
+ *   oracle_softmax_{d,f}      pipeline_code_bench/sddmm_taco_naive.cpp:191-209 (softmax over all nonzeros)
+ *   The pipeline restatements are pinned by the reference's own gold (sddmm_bench.cpp:250-280 computes the same
+ *   row-i-of-K product) and by tests/test_pipeline.py; the reference pipeline plugin itself needs Intel MKL
+ *   (absent here), so no reference build pins them bit for bit.
  *
  * Summation order: compute_csr accumulates each output entry left-to-right over the row's nonzeros, starting
  * from 0.  Compiled with the reference flags on an FMA-capable x86 (-O3 -march=...), GCC contracts
@@ -285,4 +291,57 @@ void oracle_drand48_fill(int64_t seed, double *out, int64_t n)
 		X = (0x5DEECE66DULL * X + 0xBULL) & ((1ULL << 48) - 1);
 		out[i] = ldexp((double) X, -48);
 	}
+}
+
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Pipeline SDDMM  (pipeline_code_bench/sddmm_taco_naive.cpp:98-140, 280-290)
+ *   compute_csr zeroes y, then compute2 adds, for every mask nonzero pA2 of row mA, O[mA][nD] * D[mA][nD] over nD
+ *   (O = Q, D = K, both [m][n] row-major; kA = the nonzero's column is read but not used: row mA of K), then
+ *   multiplies by the mask value.  `B += O*D` is contracted to fma by the reference flags.  mode 1 restates the
+ *   attention SDDMM the pipeline intends (row kA = col of the nonzero), same chain order.
+ * ------------------------------------------------------------------------------------------------------- */
+void oracle_sddmm_d(const int32_t *ia, const int32_t *ja, const double *a, int64_t m, const double *Q,
+                    const double *K, int32_t n, int32_t mode, double *y)
+{
+	for (int64_t i = 0; i < m; i++)
+		for (int64_t p = ia[i]; p < ia[i + 1]; p++) {
+			const int64_t kr = mode ? ja[p] : i;
+			double acc = 0;
+			for (int64_t t = 0; t < n; t++)
+				acc = fma(Q[i * n + t], K[kr * n + t], acc);
+			y[p] = acc * a[p];
+		}
+}
+
+void oracle_sddmm_f(const int32_t *ia, const int32_t *ja, const float *a, int64_t m, const float *Q,
+                    const float *K, int32_t n, int32_t mode, float *y)
+{
+	for (int64_t i = 0; i < m; i++)
+		for (int64_t p = ia[i]; p < ia[i + 1]; p++) {
+			const int64_t kr = mode ? ja[p] : i;
+			float acc = 0;
+			for (int64_t t = 0; t < n; t++)
+				acc = fmaf(Q[i * n + t], K[kr * n + t], acc);
+			y[p] = acc * a[p];
+		}
+}
+
+/* softmax over all nonzeros, serial (sddmm_taco_naive.cpp:191-209) */
+void oracle_softmax_d(double *y, int64_t nnz)
+{
+	if (nnz <= 0) return;
+	double mx = y[0], sum = 0;
+	for (int64_t i = 1; i < nnz; i++) if (y[i] > mx) mx = y[i];
+	for (int64_t i = 0; i < nnz; i++) { y[i] = exp(y[i] - mx); sum += y[i]; }
+	for (int64_t i = 0; i < nnz; i++) y[i] /= sum;
+}
+
+void oracle_softmax_f(float *y, int64_t nnz)
+{
+	if (nnz <= 0) return;
+	float mx = y[0], sum = 0;
+	for (int64_t i = 1; i < nnz; i++) if (y[i] > mx) mx = y[i];
+	for (int64_t i = 0; i < nnz; i++) { y[i] = expf(y[i] - mx); sum += y[i]; }
+	for (int64_t i = 0; i < nnz; i++) y[i] /= sum;
 }

@@ -138,6 +138,9 @@ struct spmm_hip_handle {
     uint16_t *d_tseg = nullptr, *d_tlidx = nullptr;
     void *d_tval = nullptr;
     long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
+    int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)
+    int32_t *d_tperm = nullptr;      // tile chunk-major position -> nonzero, -1 = padding (value updates re-gather tval)
+    int64_t nwperm = 0, ntperm = 0;
 
     // per-k buffers
     void *d_b = nullptr;      // row-major B [ncols][k]
@@ -184,7 +187,7 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 void free_plan(spmm_hip_t *h) {
     void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
                   h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr, h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg,
-                  h->d_tlidx, h->d_tval, h->d_tstamps};
+                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
@@ -196,6 +199,8 @@ void free_plan(spmm_hip_t *h) {
     h->d_tseg = h->d_tlidx = nullptr;
     h->d_tval = nullptr;
     h->d_tstamps = nullptr;
+    h->d_wperm = h->d_tperm = nullptr;
+    h->nwperm = h->ntperm = 0;
     h->fuse = false;
     h->win_blk.clear();
     h->win_v.clear();
@@ -1332,6 +1337,9 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         }
         if (e == hipSuccess) e = alloc_copy((void **)&h->d_wcol, wcol.data(), wcol.size() * 4);
         if (e == hipSuccess) e = alloc_copy(&h->d_wval, wval.data(), wval.size());
+        std::vector<int32_t> wp(in.perm.begin(), in.perm.end());
+        h->nwperm = (int64_t)wp.size();
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_wperm, wp.data(), wp.size() * 4);
         h->insp_bytes += wcol.size() * 4 + wval.size();
     }
     if (e == hipSuccess && tiles) {
@@ -1353,6 +1361,9 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         if (e == hipSuccess) e = alloc_copy((void **)&h->d_tseg, tp.tseg.data(), tp.tseg.size() * 2);
         if (e == hipSuccess) e = alloc_copy((void **)&h->d_tlidx, tp.tlidx.data(), tp.tlidx.size() * 2);
         if (e == hipSuccess) e = alloc_copy(&h->d_tval, tval.data(), tval.size());
+        std::vector<int32_t> tpm(tp.perm.begin(), tp.perm.end());
+        h->ntperm = (int64_t)tpm.size();
+        if (e == hipSuccess) e = alloc_copy((void **)&h->d_tperm, tpm.data(), tpm.size() * 4);
         if (e == hipSuccess && env_int("SPMM_HIP_TILE_STAMPS", 0)) {
             e = hipMalloc((void **)&h->d_tstamps, tp.tiles.size() * 4 * sizeof(long long));
             if (e == hipSuccess) e = hipMemset(h->d_tstamps, 0, tp.tiles.size() * 4 * sizeof(long long));
@@ -1402,6 +1413,84 @@ int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *
     if (ev) HIPCHK(hipEventRecord(h->ev[1], s));
     h->have_times = ev;
     h->have_copies = false;
+    return SPMM_HIP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// dst[q] = perm[q] >= 0 ? src[perm[q]] : 0 (the window-major / tile chunk-major copies of A's values)
+template <typename T>
+__global__ __launch_bounds__(WG) void gather_values_kernel(const T *__restrict__ src, const int32_t *__restrict__ perm,
+                                                           T *__restrict__ dst, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * WG + threadIdx.x;
+    if (q < n) {
+        const int32_t j = perm[q];
+        dst[q] = j >= 0 ? src[j] : T(0);
+    }
+}
+
+int update_values(spmm_hip_t *h, const void *vals, hipMemcpyKind kind, hipStream_t s) {
+    if (h->nnz == 0) return SPMM_HIP_OK;
+    HIPCHK(hipMemcpyAsync(h->d_val, vals, (size_t)h->nnz * h->vsize, kind, s));
+    auto gather = [&](const int32_t *perm, void *dst, int64_t n) -> int {
+        if (!perm || n == 0) return SPMM_HIP_OK;
+        const unsigned nb = (unsigned)((n + WG - 1) / WG);
+        if (h->dtype == SPMM_HIP_F64)
+            gather_values_kernel<double><<<nb, WG, 0, s>>>((const double *)h->d_val, perm, (double *)dst, n);
+        else
+            gather_values_kernel<float><<<nb, WG, 0, s>>>((const float *)h->d_val, perm, (float *)dst, n);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? SPMM_HIP_OK : fail(SPMM_HIP_ERR_HIP, std::string("gather launch: ") + hipGetErrorString(e));
+    };
+    if (int st = gather(h->d_wperm, h->d_wval, h->nwperm)) return st;
+    if (int st = gather(h->d_tperm, h->d_tval, h->ntperm)) return st;
+    return SPMM_HIP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int spmm_hip_update_values_device(spmm_hip_t *h, const void *d_vals, void *stream) {
+    if (!h || (!d_vals && h->nnz > 0)) return fail(SPMM_HIP_ERR_ARG, "update_values_device: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    return update_values(h, d_vals, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+}
+
+int spmm_hip_update_values(spmm_hip_t *h, const void *vals) {
+    if (!h || (!vals && h->nnz > 0)) return fail(SPMM_HIP_ERR_ARG, "update_values: bad arguments");
+    HIPCHK(hipSetDevice(h->device));
+    int st = update_values(h, vals, hipMemcpyHostToDevice, h->stream);
+    if (st != SPMM_HIP_OK) return st;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return SPMM_HIP_OK;
+}
+
+// Host buffers, B ROW-major (x[col*k + n], the layout MKL's csrmm takes in the reference pipeline plugin,
+// pipeline_code_bench/sddmm_taco_naive.cpp:219-249): upload straight into the engine's B, no transpose.
+int spmm_hip_run_rowmajor(spmm_hip_t *h, const void *x, void *y, int32_t k) {
+    if (!h || k < 1 || (!x && h->ncols > 0) || (!y && h->m > 0)) return fail(SPMM_HIP_ERR_ARG, "run_rowmajor: bad arguments");
+    if (h->plan.k != k) {
+        int st = spmm_hip_plan(h, k);
+        if (st != SPMM_HIP_OK) return st;
+    }
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    h->last_x = nullptr;
+    HIPCHK(hipEventRecord(h->ev[4], s));
+    if (h->ncols > 0) HIPCHK(hipMemcpyAsync(h->d_b, x, (size_t)h->ncols * k * h->vsize, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(h->ev[5], s));
+    HIPCHK(hipEventRecord(h->ev[0], s));
+    if (h->m > 0) {
+        int st = launch_spmm(h, h->d_b, h->d_c, k, s);
+        if (st != SPMM_HIP_OK) return st;
+    }
+    HIPCHK(hipEventRecord(h->ev[1], s));
+    if (h->m > 0) HIPCHK(hipMemcpyAsync(y, h->d_c, (size_t)h->m * k * h->vsize, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(h->ev[6], s));
+    HIPCHK(hipStreamSynchronize(s));
+    h->have_times = h->have_copies = true;
+    h->have_transpose = false;
     return SPMM_HIP_OK;
 }
 

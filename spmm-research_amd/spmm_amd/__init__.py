@@ -121,6 +121,14 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_debug_free.argtypes = [C.POINTER(_Inspection)]
     L.spmm_hip_debug_free.restype = None
     L.spmm_hip_tile_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
+    L.spmm_hip_run_rowmajor.argtypes = [vp, vp, vp, i32]
+    L.spmm_hip_update_values.argtypes = [vp, vp]
+    L.spmm_hip_update_values_device.argtypes = [vp, vp, vp]
+    L.spmm_sddmm_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, i32, C.POINTER(vp)]
+    L.spmm_sddmm_run.argtypes = [vp, vp, vp, i64, vp]
+    L.spmm_sddmm_run_device.argtypes = [vp, vp, vp, vp, vp]
+    L.spmm_sddmm_destroy.argtypes = [vp]
+    L.spmm_sddmm_last_error_detail.restype = C.c_char_p
     L.spmm_hip_debug_tiles.argtypes = [_i32p, _i32p, i64, i64, i32, i32, i32, i32, C.c_double, i32, i32,
                                        C.POINTER(_Tiles)]
     L.spmm_hip_debug_tiles_free.argtypes = [C.POINTER(_Tiles)]
@@ -393,6 +401,26 @@ class MatrixFormat:
         if x.size < self.n * k or y.size < self.m * k or not (x.flags.c_contiguous and y.flags.c_contiguous):
             raise ValueError("x must hold n*k and y m*k contiguous values")
         _check("spmm", hip.spmm_hip_run(self._h, x.ctypes.data_as(C.c_void_p), y.ctypes.data_as(C.c_void_p), k))
+
+    def spmm_rowmajor(self, x: np.ndarray, y: np.ndarray, k: int) -> None:
+        """Host x ROW-major [n][k] (the pipeline plugin's MKL layout), host y row-major [m][k]."""
+        if x.dtype != self.dtype or y.dtype != self.dtype:
+            raise TypeError("x and y must have the handle's ValueType")
+        if x.size < self.n * k or y.size < self.m * k or not (x.flags.c_contiguous and y.flags.c_contiguous):
+            raise ValueError("x must hold n*k and y m*k contiguous values")
+        _check("spmm_rowmajor", hip.spmm_hip_run_rowmajor(self._h, x.ctypes.data_as(C.c_void_p),
+                                                          y.ctypes.data_as(C.c_void_p), k))
+
+    def update_values(self, vals: np.ndarray) -> None:
+        """Replace A's values (same pattern), host array."""
+        v = np.ascontiguousarray(vals, self.dtype)
+        if v.size < self.nnz:
+            raise ValueError("need nnz values")
+        _check("update_values", hip.spmm_hip_update_values(self._h, v.ctypes.data_as(C.c_void_p)))
+
+    def update_values_device(self, d_vals: int, stream: int = 0) -> None:
+        _check("update_values_device", hip.spmm_hip_update_values_device(self._h, C.c_void_p(d_vals),
+                                                                         C.c_void_p(stream)))
 
     def spmm_device(self, d_b: int, b_layout: int, d_c: int, k: int, stream: int = 0) -> None:
         """HBM-resident run: d_b / d_c are device addresses (e.g. torch tensor .data_ptr())."""
