@@ -96,7 +96,13 @@ int spmm_host_mtx_read(const char *path, spmm_csr_t *out, char *field_out, int f
  * values, so they are a seeded uniform [-1, 1) stream (the reference's are time-seeded rand(), unreproducible). */
 int spmm_host_smtx_read(const char *path, int64_t value_seed, spmm_csr_t *out);
 
-int spmm_host_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t nnz,
+/* coo_to_csr(R, C, V, m, n, nnz, row_ptr, col_idx, values, sort_columns=1, transpose=0) (csr_gen.c:163-217):
+ * rows bucketed, each row sorted by column, duplicates kept.  Duplicate (row, col) values keep the order the
+ * reference leaves when run by one OpenMP thread (file entries reversed by the row bucketing, then its per-row
+ * sort: stable bucket sort for rows of more than n/5 entries, its quicksort otherwise); with several threads the
+ * reference's own order among duplicates depends on thread timing (atomic slot hand-out, bucketsort_gen.c:186-194).
+ * V may be NULL (values 1.0). */
+int spmm_host_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t n, int64_t nnz,
                          int32_t *row_ptr, int32_t *col_idx, double *values);
 
 void spmm_host_csr_free(spmm_csr_t *a);

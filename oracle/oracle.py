@@ -49,7 +49,7 @@ def lib() -> C.CDLL:
         L.oracle_gold_to_double.argtypes = [_i32p, _i32p, _f64p, i64, i64, _f64p, C.c_int32, _f64p, C.c_void_p]
         L.oracle_gold.argtypes = [_i32p, _i32p, _f64p, i64, i64, _f64p, C.c_int32, C.c_void_p]
         L.oracle_check_accuracy.argtypes = [C.c_void_p, _f64p, i64, C.c_double, _f64p]
-        L.oracle_coo_to_csr.argtypes = [_i32p, _i32p, C.c_void_p, i64, i64, _i32p, _i32p, _f64p]
+        L.oracle_coo_to_csr.argtypes = [_i32p, _i32p, C.c_void_p, i64, i64, i64, _i32p, _i32p, _f64p]
         L.oracle_drand48_fill.argtypes = [i64, _f64p, i64]
         L.oracle_sddmm_d.argtypes = [_i32p, _i32p, _f64p, i64, _f64p, _f64p, C.c_int32, C.c_int32, _f64p]
         L.oracle_sddmm_f.argtypes = [_i32p, _i32p, _f32p, i64, _f32p, _f32p, C.c_int32, C.c_int32, _f32p]
@@ -75,6 +75,8 @@ def ref_lib(vt: str = "d") -> C.CDLL:
         L.ref_mtx_to_csr.argtypes = [C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_long),
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ref_free.argtypes = [C.c_void_p]
+        L.ref_smtx_read.argtypes = [C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_long),
+                                    C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ref_partition.argtypes = [_i32p, C.c_long, C.c_long, C.c_long, C.c_long, C.POINTER(C.c_long),
                                     C.POINTER(C.c_long)]
         L.ref_metrics.argtypes = [_f64p, _f64p, C.c_long, _f64p]
@@ -126,14 +128,17 @@ def check_accuracy(row_ptr, col_idx, vals_ref, ncols: int, x_ref_colmajor, k: in
     return out
 
 
-def coo_to_csr(R, Cc, V, m: int):
+def coo_to_csr(R, Cc, V, m: int, n: int | None = None):
+    """coo_to_csr (csr_gen.c:163-217) as the reference runs it with one thread; n = column count (default
+    max column + 1)."""
     nnz = len(R)
+    Cc = np.ascontiguousarray(Cc, np.int32)
+    ncols = (int(Cc.max()) + 1 if nnz else 0) if n is None else int(n)
     rp = np.empty(m + 1, np.int32)
     ci = np.empty(max(nnz, 1), np.int32)
     va = np.empty(max(nnz, 1), np.float64)
     vptr = None if V is None else np.ascontiguousarray(V, np.float64).ctypes.data_as(C.c_void_p)
-    lib().oracle_coo_to_csr(np.ascontiguousarray(R, np.int32), np.ascontiguousarray(Cc, np.int32), vptr, m, nnz,
-                            rp, ci, va)
+    lib().oracle_coo_to_csr(np.ascontiguousarray(R, np.int32), Cc, vptr, m, ncols, nnz, rp, ci, va)
     return rp, ci[:nnz], va[:nnz]
 
 
@@ -239,3 +244,16 @@ def spmm_rowmajor(row_ptr, col_idx, vals, ncols: int, x_rowmajor: np.ndarray) ->
     x = np.asarray(x_rowmajor)
     n = x.shape[1]
     return spmm(row_ptr, col_idx, vals, ncols, np.ascontiguousarray(x.T).ravel(), n)
+
+
+def ref_smtx_read(path: str, vt: str = "d"):
+    """The reference's DLMC reader (dlcm_matrix.c:258-324): (m, k, row_ptr, col_idx) as stored."""
+    L = ref_lib(vt)
+    m, k, nnz = C.c_long(), C.c_long(), C.c_long()
+    rp, ci = C.c_void_p(), C.c_void_p()
+    assert L.ref_smtx_read(path.encode(), C.byref(m), C.byref(k), C.byref(nnz), C.byref(rp), C.byref(ci)) == 0
+    r = np.ctypeslib.as_array(C.cast(rp, C.POINTER(C.c_int32)), (m.value + 1,)).copy()
+    c = np.ctypeslib.as_array(C.cast(ci, C.POINTER(C.c_int32)), (max(nnz.value, 1),))[:nnz.value].copy()
+    L.ref_free(rp)
+    L.ref_free(ci)
+    return m.value, k.value, r, c

@@ -10,6 +10,7 @@
  *   ref_spmm         csr_to_format(...)->spmm(x, y, k)  (spmv_bench.cpp:996, :372 -> spmm_kernel_csr.cpp:51-96)
  *   ref_mtx_to_csr   mtx_read + field conversion + coo_to_csr(..., sort_columns=1, transpose=0)
  *                    (spmv_bench.cpp:724-763 and :805-826)
+ *   ref_smtx_read    DLMC smtx_read (lib/storage_formats/dlcm_matrices/dlcm_matrix.c:258-324), offsets and columns
  *   ref_partition    loop_partitioner_balance_prefix_sums (lib/parallel_util.h:141-165)
  *   ref_metrics      the 8 array_metrics calls of CheckAccuracy (spmv_bench.cpp:189-203)
  *   ref_features     csr_matrix_features_validation (lib/storage_formats/csr_util/csr_util_gen.c:889-990, built as
@@ -34,6 +35,7 @@ extern "C" {
 #include "storage_formats/matrix_market/matrix_market.h"
 #include "aux/csr_converter_double.h"
 #include "aux/csr_util.h"
+#include "storage_formats/dlcm_matrices/dlcm_matrix.h"
 }
 #include <unistd.h>
 
@@ -96,6 +98,21 @@ void ref_spmm(INT_T *row_ptr, INT_T *col_idx, ValueType *values, long m, long n,
 	struct Matrix_Format *MF = csr_to_format(row_ptr, col_idx, values, m, n, nnz, k);
 	MF->spmm(x, y, k);
 	delete MF;
+}
+
+/* Reads a DLMC .smtx file with the reference's smtx_read (dlcm_matrix.c:258-324): row offsets and column indices
+ * as stored (the harness copies them without coo_to_csr, spmv_bench.cpp:667-696,769-801).  Its values are
+ * time-seeded rand() and are not returned.  Arrays malloc'ed (ref_free). */
+int ref_smtx_read(char *path, long *m_out, long *k_out, long *nnz_out, INT_T **row_ptr_out, INT_T **col_idx_out)
+{
+	struct DLCM_Matrix *MTX = smtx_read(path, 1, 1);
+	*m_out = MTX->m;
+	*k_out = MTX->k;
+	*nnz_out = MTX->nnz;
+	*row_ptr_out = (INT_T *) MTX->R;
+	*col_idx_out = (INT_T *) MTX->C;
+	free(MTX->V);
+	return 0;
 }
 
 /* Reads a .mtx file the way the harness does.  Returns 0 on success; arrays are malloc'ed (free with

@@ -243,42 +243,106 @@ void oracle_check_accuracy(const __float128 *y_gold, const double *y_test, int64
 }
 
 /* ---------------------------------------------------------------------------------------------------------
- * coo_to_csr(R, C, V, m, n, nnz, row_ptr, col_idx, values, sort_columns=1, transpose=0)  (csr_gen.c:163-217)
- * Rows bucketed (counting sort keeps the COO order of entries within a row), then each row's entries sorted by
- * column.  Duplicates are kept, not summed.  Indexing (row_ptr, col_idx) is what the parity tests pin
- * bit-for-bit; among duplicate (row, col) entries the reference's per-row quicksort (csr_gen.c:132) is not
- * stable, so their value order is not pinned -- this restatement keeps COO order (stable).
+ * coo_to_csr(R, C, V, m, n, nnz, row_ptr, col_idx, values, sort_columns=1, transpose=0)  (csr_gen.c:163-217),
+ * as the reference runs it with ONE OpenMP thread:
+ *  - bucketsort by row (lib/sort/bucketsort/bucketsort_gen.c:163-199): counts, inclusive scan, then entry i takes
+ *    slot --end[row] -- each row holds its COO entries in reverse order.  (With several threads the slots are
+ *    handed out by an atomic decrement in whatever order the threads arrive: the reference's order among duplicate
+ *    (row, col) entries is then not reproducible.)
+ *  - csr_sort_columns (csr_gen.c:83-156) per row: degree > n/5 -> stable bucket sort by column
+ *    (bucketsort_stable_serial, bucketsort_gen.c:127-160); otherwise quicksort of the entry indices keyed by column
+ *    (quicksort_gen.c:93-127: partition [s, e], push s, continue right; when a part is one element, e-- and pop),
+ *    partitions by partition_auto_serial (partition_gen.c:269-294: sizes 1 and 2 directly, else median of three
+ *    at s, (s+e)/2, e, then partition_serial_base (:146-193) of [s+1, e-1] around the middle entry).
+ * Indexing does not depend on any of this; the VALUE order among duplicates does, and is pinned against the
+ * reference run with one thread (tests/golden/make_golden.py sets it).
  * ------------------------------------------------------------------------------------------------------- */
-typedef struct { int32_t col; int64_t pos; } oracle_ent_t;
-
-static int ent_cmp(const void *pa, const void *pb)
+static int qs_cmp(int32_t a, int32_t b, const int32_t *key)
 {
-	const oracle_ent_t *a = (const oracle_ent_t *) pa, *b = (const oracle_ent_t *) pb;
-	if (a->col != b->col) return (a->col < b->col) ? -1 : 1;
-	return (a->pos < b->pos) ? -1 : (a->pos > b->pos);
+	return (key[a] > key[b]) ? 1 : (key[a] < key[b]) ? -1 : 0;
 }
 
-void oracle_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t nnz,
+static int64_t qs_partition_base(int32_t pivot, int32_t *A, int64_t lo, int64_t hi, const int32_t *key)
+{
+	while (1) {
+		while (lo < hi && qs_cmp(A[lo], pivot, key) < 0) lo++;
+		while (lo < hi && qs_cmp(A[hi], pivot, key) > 0) hi--;
+		if (lo >= hi) break;
+		int32_t t = A[lo]; A[lo] = A[hi]; A[hi] = t;
+		lo++; hi--;
+	}
+	if (qs_cmp(A[lo], pivot, key) < 0) lo++;
+	return lo;
+}
+
+#define QS_SWAP(x, y) do { int32_t _t = (x); (x) = (y); (y) = _t; } while (0)
+
+static int64_t qs_partition_auto(int32_t *A, int64_t s, int64_t e_excl, const int32_t *key)
+{
+	if (e_excl - s == 1) return s;
+	if (e_excl - s == 2) {
+		if (qs_cmp(A[s], A[s + 1], key) > 0) QS_SWAP(A[s], A[s + 1]);
+		return s + 1;
+	}
+	int64_t e = e_excl - 1, p = (s + e) / 2;
+	if (qs_cmp(A[s], A[e], key) > 0) QS_SWAP(A[s], A[e]);
+	if (qs_cmp(A[s], A[p], key) > 0) QS_SWAP(A[s], A[p]);
+	if (qs_cmp(A[p], A[e], key) > 0) QS_SWAP(A[p], A[e]);
+	return qs_partition_base(A[p], A, s + 1, e - 1, key);
+}
+
+static void qs_sort(int32_t *A, int64_t N, const int32_t *key, int64_t *parts)
+{
+	if (N < 2) return;
+	int64_t s = 0, e = N - 1, i = 0;
+	while (1) {
+		while (s >= e) {
+			if (s == 0) return;
+			i--;
+			e--;
+			s = parts[i];
+		}
+		int64_t mid = qs_partition_auto(A, s, e + 1, key);
+		parts[i++] = s;
+		s = mid;
+	}
+}
+
+void oracle_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t n, int64_t nnz,
                        int32_t *row_ptr, int32_t *col_idx, double *values)
 {
-	int64_t *cnt = (int64_t *) calloc(m + 1, sizeof(int64_t));
-	int64_t *fill = (int64_t *) malloc((m + 1) * sizeof(int64_t));
-	oracle_ent_t *ent = (oracle_ent_t *) malloc((nnz > 0 ? nnz : 1) * sizeof(oracle_ent_t));
-	for (int64_t i = 0; i < nnz; i++) cnt[R[i] + 1]++;
-	for (int64_t i = 0; i < m; i++) cnt[i + 1] += cnt[i];
-	for (int64_t i = 0; i <= m; i++) { row_ptr[i] = (int32_t) cnt[i]; fill[i] = cnt[i]; }
-	for (int64_t i = 0; i < nnz; i++) {
-		int64_t p = fill[R[i]]++;
-		ent[p].col = C[i];
-		ent[p].pos = i;
+	int64_t *end = (int64_t *) calloc(m + 1, sizeof(int64_t));
+	int32_t *Cb = (int32_t *) malloc((nnz > 0 ? nnz : 1) * sizeof(int32_t));
+	double *Vb = (double *) malloc((nnz > 0 ? nnz : 1) * sizeof(double));
+	int32_t *perm = (int32_t *) malloc((nnz > 0 ? nnz : 1) * sizeof(int32_t));
+	int64_t *parts = (int64_t *) malloc((nnz + 1) * sizeof(int64_t));
+	int64_t *cnt = (int64_t *) calloc((n > 0 ? n : 1) + 1, sizeof(int64_t));
+	for (int64_t i = 0; i < nnz; i++) end[R[i] + 1]++;
+	for (int64_t i = 0; i < m; i++) end[i + 1] += end[i];
+	for (int64_t i = 0; i <= m; i++) row_ptr[i] = (int32_t) end[i];
+	for (int64_t i = 0; i < nnz; i++) {                 /* one thread: slots handed out from each row's end */
+		int64_t p = --end[R[i] + 1];
+		Cb[p] = C[i];
+		Vb[p] = V ? V[i] : 1.0;
 	}
-	for (int64_t i = 0; i < m; i++)
-		qsort(ent + cnt[i], cnt[i + 1] - cnt[i], sizeof(oracle_ent_t), ent_cmp);
-	for (int64_t p = 0; p < nnz; p++) {
-		col_idx[p] = ent[p].col;
-		if (values) values[p] = V ? V[ent[p].pos] : 1.0;
+	for (int64_t i = 0; i < m; i++) {
+		int64_t s = row_ptr[i], deg = row_ptr[i + 1] - s;
+		if (deg == 0) continue;
+		if (deg > n / 5) {                               /* stable bucket sort by column */
+			for (int64_t q = 0; q < deg; q++) cnt[Cb[s + q] + 1]++;
+			for (int64_t c = 0; c < n; c++) cnt[c + 1] += cnt[c];
+			for (int64_t q = 0; q < deg; q++) perm[cnt[Cb[s + q]]++] = (int32_t) q;
+			memset(cnt, 0, ((n > 0 ? n : 1) + 1) * sizeof(int64_t));
+		} else {
+			for (int64_t q = 0; q < deg; q++) perm[q] = (int32_t) q;
+			qs_sort(perm, deg, Cb + s, parts);
+		}
+		for (int64_t q = 0; q < deg; q++) {
+			col_idx[s + q] = Cb[s + perm[q]];
+			if (values) values[s + q] = Vb[s + perm[q]];
+		}
 	}
-	free(cnt); free(fill); free(ent);
+	free(end); free(Cb); free(Vb); free(perm); free(parts); free(cnt);
 }
 
 /* drand48 stream (POSIX: X_{n+1} = (0x5DEECE66D X_n + 0xB) mod 2^48, srand48(s): X = s<<16 | 0x330E), used

@@ -7,9 +7,13 @@
 //                   the mirrored off-diagonal entries are APPENDED after all file entries, in file order, with
 //                   value v (symmetric), -v (skew), conj(v) (Hermitian)
 //   field values    spmv_bench.cpp:730-763: integer -> double, complex -> |z|, pattern -> 1.0
-//   coo_to_csr      csr_gen.c:163-217: rows bucketed, then each row's entries sorted by column; duplicates kept
-// The one deliberate difference: among duplicate (row, col) entries the reference's per-row quicksort is not
-// stable; we keep file order (stable), so duplicate VALUES may sit in a different order (indexing is identical).
+//   coo_to_csr      csr_gen.c:163-217: rows bucketed, then each row's entries sorted by column; duplicates kept.
+//                   The order of DUPLICATE (row, col) values follows the reference run by one OpenMP thread: its row
+//                   bucketing (bucketsort_gen.c:163-199) hands slots out from the end of each row with an atomic
+//                   decrement, so with several threads the order among duplicates depends on thread timing (not
+//                   reproducible even by the reference); with one thread a row holds its file entries reversed, and
+//                   the per-row column sort (stable bucket sort for rows longer than n/5, the reference quicksort
+//                   otherwise) is restated exactly, so duplicate values come out in the reference's order.
 // "array" format (dense, column-major) is read as a full coordinate listing (the reference would dereference a
 // NULL row array there).
 #include <algorithm>
@@ -60,34 +64,117 @@ int read_lines(const char *path, Lines &L) {
     return SPMM_HOST_OK;
 }
 
+// csr_sort_columns' per-row sorts (csr_gen.c:120-140), restated.  Rows of more than n/5 entries: a stable bucket
+// sort by column (bucketsort_stable_serial, bucketsort_gen.c:127-160).  Shorter rows: the reference quicksort of
+// the entries' indices keyed by column (quicksort_gen.c:93-127 with partition_auto_serial / partition_serial_base,
+// partition_gen.c:146-193,269-294 and the comparator csr_gen.c:33-37) -- deterministic (its srandom_r state is
+// never read) but not stable, so the order it leaves among duplicate columns is its own; restated step by step.
+void ref_bucket_stable(const int32_t *cols, int64_t deg, int32_t *src_of_slot) {
+    std::vector<int64_t> idx((size_t)deg);
+    for (int64_t q = 0; q < deg; ++q) idx[(size_t)q] = q;
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return cols[a] < cols[b]; });
+    for (int64_t q = 0; q < deg; ++q) src_of_slot[q] = (int32_t)idx[(size_t)q];
+}
+
+inline int qcmp(int32_t a, int32_t b, const int32_t *keys) {
+    return keys[a] > keys[b] ? 1 : keys[a] < keys[b] ? -1 : 0;
+}
+
+// entries [lo, hi] (inclusive) around `pivot`: returns the first index of the right part
+int64_t part_base(int32_t pivot, int32_t *A, int64_t lo, int64_t hi, const int32_t *keys) {
+    for (;;) {
+        while (lo < hi && qcmp(A[lo], pivot, keys) < 0) ++lo;
+        while (lo < hi && qcmp(A[hi], pivot, keys) > 0) --hi;
+        if (lo >= hi) break;
+        std::swap(A[lo], A[hi]);
+        ++lo;
+        --hi;
+    }
+    if (qcmp(A[lo], pivot, keys) < 0) ++lo;
+    return lo;
+}
+
+// [s, e) with a median-of-three pivot at the middle
+int64_t part_auto(int32_t *A, int64_t s, int64_t e, const int32_t *keys) {
+    if (e - s == 1) return s;
+    if (e - s == 2) {
+        if (qcmp(A[s], A[s + 1], keys) > 0) std::swap(A[s], A[s + 1]);
+        return s + 1;
+    }
+    const int64_t last = e - 1, mid = (s + last) / 2;
+    if (qcmp(A[s], A[last], keys) > 0) std::swap(A[s], A[last]);
+    if (qcmp(A[s], A[mid], keys) > 0) std::swap(A[s], A[mid]);
+    if (qcmp(A[mid], A[last], keys) > 0) std::swap(A[mid], A[last]);
+    return part_base(A[mid], A, s + 1, last - 1, keys);
+}
+
+// the reference's iterative driver: partition [s, e], remember s, continue with the right part; when a part is
+// down to one element, step e back by one and resume from the remembered start
+void ref_quicksort(int32_t *A, int64_t N, const int32_t *keys, std::vector<int64_t> &stack) {
+    if (N < 2) return;
+    stack.assign((size_t)N + 1, 0);
+    int64_t s = 0, e = N - 1, i = 0;
+    for (;;) {
+        while (s >= e) {
+            if (s == 0) return;
+            --i;
+            --e;
+            s = stack[(size_t)i];
+        }
+        const int64_t m = part_auto(A, s, e + 1, keys);
+        stack[(size_t)i++] = s;
+        s = m;
+    }
+}
+
 }  // namespace
 
 extern "C" {
 
-int spmm_host_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t nnz,
+int spmm_host_coo_to_csr(const int32_t *R, const int32_t *C, const double *V, int64_t m, int64_t n, int64_t nnz,
                          int32_t *row_ptr, int32_t *col_idx, double *values) {
-    if (m < 0 || nnz < 0 || !row_ptr || (nnz > 0 && (!R || !C || !col_idx))) return SPMM_HOST_ERR_ARG;
+    if (m < 0 || n < 0 || nnz < 0 || !row_ptr || (nnz > 0 && (!R || !C || !col_idx))) return SPMM_HOST_ERR_ARG;
     if (nnz >= INT32_MAX) return SPMM_HOST_ERR_OVERFLOW;
-    std::vector<int64_t> cnt((size_t)m + 1, 0);
+    std::vector<int64_t> end((size_t)m + 1, 0);
     for (int64_t i = 0; i < nnz; ++i) {
-        if (R[i] < 0 || R[i] >= m) return SPMM_HOST_ERR_ARG;
-        cnt[R[i] + 1]++;
+        if (R[i] < 0 || R[i] >= m || C[i] < 0 || C[i] >= n) return SPMM_HOST_ERR_ARG;
+        end[R[i] + 1]++;
     }
-    for (int64_t i = 0; i < m; ++i) cnt[i + 1] += cnt[i];
-    for (int64_t i = 0; i <= m; ++i) row_ptr[i] = (int32_t)cnt[i];
-    std::vector<int64_t> perm((size_t)nnz);
+    for (int64_t i = 0; i < m; ++i) end[i + 1] += end[i];
+    for (int64_t i = 0; i <= m; ++i) row_ptr[i] = (int32_t)end[i];
+    // 1. rows bucketed like the reference's bucketsort (bucketsort_gen.c:163-199) run by ONE thread: each entry
+    //    takes the next free slot from the END of its row, so a row holds its file entries in reverse order
+    std::vector<int32_t> Cb((size_t)nnz);
+    std::vector<double> Vb((size_t)nnz);
     {
-        std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
-        for (int64_t i = 0; i < nnz; ++i) perm[fill[R[i]]++] = i;  // stable bucket by row
+        std::vector<int64_t> top(end.begin() + 1, end.end());
+        for (int64_t i = 0; i < nnz; ++i) {
+            const int64_t pos = --top[R[i]];
+            Cb[(size_t)pos] = C[i];
+            Vb[(size_t)pos] = V ? V[i] : 1.0;
+        }
     }
-#pragma omp parallel for schedule(dynamic, 1024)
-    for (int64_t i = 0; i < m; ++i)
-        std::stable_sort(perm.begin() + cnt[i], perm.begin() + cnt[i + 1],
-                         [&](int64_t a, int64_t b) { return C[a] < C[b]; });
-#pragma omp parallel for schedule(static)
-    for (int64_t p = 0; p < nnz; ++p) {
-        col_idx[p] = C[perm[p]];
-        if (values) values[p] = V ? V[perm[p]] : 1.0;
+    // 2. each row sorted by column (csr_sort_columns, csr_gen.c:83-156)
+#pragma omp parallel
+    {
+        std::vector<int32_t> perm;
+        std::vector<int64_t> stack;
+#pragma omp for schedule(dynamic, 256)
+        for (int64_t i = 0; i < m; ++i) {
+            const int64_t s = end[i], deg = end[i + 1] - s;
+            if (deg == 0) continue;
+            perm.resize((size_t)deg);
+            if (deg > n / 5) {
+                ref_bucket_stable(Cb.data() + s, deg, perm.data());      // perm[q] = source of slot q
+            } else {
+                for (int64_t q = 0; q < deg; ++q) perm[(size_t)q] = (int32_t)q;
+                ref_quicksort(perm.data(), deg, Cb.data() + s, stack);
+            }
+            for (int64_t q = 0; q < deg; ++q) {
+                col_idx[s + q] = Cb[(size_t)(s + perm[(size_t)q])];
+                if (values) values[s + q] = Vb[(size_t)(s + perm[(size_t)q])];
+            }
+        }
     }
     return SPMM_HOST_OK;
 }
@@ -208,7 +295,7 @@ int spmm_host_mtx_read(const char *path, spmm_csr_t *out, char *field_out, int f
         spmm_host_csr_free(out);
         return SPMM_HOST_ERR_NOMEM;
     }
-    st = spmm_host_coo_to_csr(R.data(), C.data(), V.data(), M, nnz, out->row_ptr, out->col_idx, out->values);
+    st = spmm_host_coo_to_csr(R.data(), C.data(), V.data(), M, N, nnz, out->row_ptr, out->col_idx, out->values);
     if (st) {
         spmm_host_csr_free(out);
         return st;

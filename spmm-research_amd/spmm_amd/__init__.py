@@ -150,7 +150,7 @@ def _bind_host(L: C.CDLL) -> C.CDLL:
     L.spmm_host_features.argtypes = [C.POINTER(_CSRStruct), C.POINTER(_Features)]
     L.spmm_host_mtx_read.argtypes = [C.c_char_p, C.POINTER(_CSRStruct), C.c_char_p, C.c_int, C.POINTER(C.c_int32)]
     L.spmm_host_smtx_read.argtypes = [C.c_char_p, i64, C.POINTER(_CSRStruct)]
-    L.spmm_host_coo_to_csr.argtypes = [_i32p, _i32p, vp, i64, i64, _i32p, _i32p, _f64p]
+    L.spmm_host_coo_to_csr.argtypes = [_i32p, _i32p, vp, i64, i64, i64, _i32p, _i32p, _f64p]
     L.spmm_host_csr_free.argtypes = [C.POINTER(_CSRStruct)]
     L.spmm_host_drand48_fill.argtypes = [i64, _f64p, i64]
     L.spmm_host_uniform_fill.argtypes = [i64, C.c_double, C.c_double, _f64p, i64]
@@ -267,18 +267,20 @@ def smtx_read(path: str | os.PathLike, value_seed: int = 42) -> CSR:
     return _take_csr(s)
 
 
-def coo_to_csr(R, Cc, V, m: int) -> CSR:
+def coo_to_csr(R, Cc, V, m: int, n: int | None = None) -> CSR:
+    """coo_to_csr (csr_gen.c:163-217) with the reference's one-thread duplicate order; n = column count
+    (default max column + 1)."""
     R = np.ascontiguousarray(R, np.int32)
     Cc = np.ascontiguousarray(Cc, np.int32)
     nnz = len(R)
+    ncols = (int(Cc.max()) + 1 if nnz else 0) if n is None else int(n)
     rp = np.empty(m + 1, np.int32)
     ci = np.empty(max(nnz, 1), np.int32)
     va = np.empty(max(nnz, 1), np.float64)
     vptr = None if V is None else np.ascontiguousarray(V, np.float64).ctypes.data_as(C.c_void_p)
-    st = host.spmm_host_coo_to_csr(R, Cc, vptr, m, nnz, rp, ci, va)
+    st = host.spmm_host_coo_to_csr(R, Cc, vptr, m, ncols, nnz, rp, ci, va)
     if st != 0:
         raise ValueError(f"coo_to_csr failed ({st})")
-    ncols = int(Cc.max()) + 1 if nnz else 0
     return CSR(rp, ci[:nnz], va[:nnz], m, ncols)
 
 

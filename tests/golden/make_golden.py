@@ -7,6 +7,7 @@ What it writes (data only -- inputs and the reference's outputs; no reference so
   mtx/*.mtx                 hand-written Matrix Market inputs covering the reader's cases
                             (general/symmetric/skew/Hermitian; real/integer/complex/pattern; empty rows; duplicates;
                             one long row; unsorted entries)
+  smtx_csr.npz              per DLMC .smtx (tests/golden/smtx/): the offsets / columns smtx_read returns
   mtx_csr.npz               per .mtx: the CSR that mtx_read + coo_to_csr produce (spmv_bench.cpp:724-826), and
                             C = A*B from the reference plugin for K in {1,4,32} with B = 1 and B = drand48(42)
   spmm_cases.npz            seeded random CSRs (empty rows, a long row, a zero-nnz matrix) and the reference
@@ -140,6 +141,9 @@ def b_inputs(ncols: int, k: int):
 
 
 def make_mtx_fixtures():
+    # one OpenMP thread: the reference's row bucketing hands out slots by atomic decrement, so with several threads
+    # the order of duplicate (row, col) values depends on thread timing (bucketsort_gen.c:186-194)
+    O.ref_lib("d").ref_set_threads(1)
     out = {}
     for name in sorted(MTX_FILES):
         m, n, rp, ci, va = O.ref_mtx_to_csr(str(MTX / name), "d")
@@ -153,6 +157,43 @@ def make_mtx_fixtures():
                 y = O.ref_spmm(rp, ci, va.copy(), n, x, k)
                 out[f"{key}.y.k{k}.{bname}"] = y
     np.savez_compressed(OUT / "mtx_csr.npz", **out)
+
+
+SMTX = ROOT / "tests" / "golden" / "smtx"
+
+
+def make_smtx_fixtures():
+    """DLMC .smtx inputs (the USE_DLCM_MATRICES path) and the row offsets / columns the reference's smtx_read
+    returns (dlcm_matrix.c:258-324; values are time-seeded there, not pinned)."""
+    SMTX.mkdir(exist_ok=True)
+    rng = np.random.default_rng(21)
+    files = {}
+    # a transformer-like pruned weight (rows sorted), one with unsorted rows and duplicates, empty rows, one row
+    for name, (m, k, dens, shuffle) in {"pruned_64x48": (64, 48, 0.3, False), "unsorted_dups": (40, 30, 0.2, True),
+                                        "empty_rows": (25, 60, 0.05, False), "one_row": (1, 17, 0.5, False)}.items():
+        deg = rng.binomial(k, dens, m)
+        if name == "empty_rows":
+            deg[::3] = 0
+        rows = []
+        for d in deg:
+            c = np.sort(rng.choice(k, d, replace=False))
+            if shuffle and d > 1:
+                c = np.concatenate([c, c[: max(1, d // 4)]])      # duplicates
+                rng.shuffle(c)
+            rows.append(c)
+        rp = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+        ci = np.concatenate(rows).astype(np.int32) if rows else np.zeros(0, np.int32)
+        text = f"{m}, {k}, {len(ci)}\n" + " ".join(map(str, rp)) + "\n" + " ".join(map(str, ci)) + "\n"
+        files[name] = text
+    out = {}
+    for name, text in files.items():
+        path = SMTX / f"{name}.smtx"
+        path.write_text(text)
+        m, k, rp, ci = O.ref_smtx_read(str(path))
+        out[f"{name}.shape"] = np.array([m, k], np.int64)
+        out[f"{name}.row_ptr"] = rp
+        out[f"{name}.col_idx"] = ci
+    np.savez_compressed(OUT / "smtx_csr.npz", **out)
 
 
 def random_csr(rng, m, n, mean_deg, long_row=None, empty_frac=0.1):
@@ -283,6 +324,7 @@ def main():
         raise SystemExit("oracle/_ref not built: run `make -C oracle` in a container with /root/reference")
     write_mtx()
     make_mtx_fixtures()
+    make_smtx_fixtures()
     make_spmm_cases()
     make_partition()
     make_metrics()

@@ -22,13 +22,8 @@ def test_mtx_reader_matches_reference_indexing(golden):
         assert (A.m, A.ncols) == (m, n), c
         assert np.array_equal(A.row_ptr, d[f"{c}.row_ptr"]), c
         assert np.array_equal(A.col_idx, d[f"{c}.col_idx"]), c
-        # values: equal per (row, col) as multisets (the reference's per-row quicksort is not stable for duplicates)
-        want = d[f"{c}.vals"]
-        for i in range(m):
-            a, b = A.row_ptr[i], A.row_ptr[i + 1]
-            for col in np.unique(A.col_idx[a:b]):
-                sel = A.col_idx[a:b] == col
-                assert sorted(A.values[a:b][sel]) == sorted(want[a:b][sel]), (c, i, col)
+        # values bit for bit, duplicates included (the reference's one-thread order, tests/golden/make_golden.py)
+        assert np.array_equal(A.values.view(np.int64), d[f"{c}.vals"].view(np.int64)), c
 
 
 def test_mtx_reader_rejects_malformed(tmp_path):
@@ -51,7 +46,7 @@ def write_smtx(path, rp, ci, m, n):
 
 def test_smtx_reader_keeps_stored_csr(tmp_path):
     """USE_DLCM_MATRICES path: offsets and columns used exactly as stored (no coo_to_csr, no column sort),
-    values a seeded U[-1, 1) stream.  No .smtx fixture exists in the reference, so the round trip is synthetic."""
+    values a seeded U[-1, 1) stream (the reference seeds from time(NULL), so values are not pinnable)."""
     rng = np.random.default_rng(3)
     m, n = 37, 53
     deg = rng.integers(0, 9, m)
@@ -69,6 +64,40 @@ def test_smtx_reader_keeps_stored_csr(tmp_path):
     e.write_text("4, 6, 0\n0 0 0 0 0\n")
     E = S.smtx_read(e)
     assert (E.m, E.ncols, E.nnz) == (4, 6, 0) and np.array_equal(E.row_ptr, np.zeros(5, np.int32))
+
+
+def test_smtx_reader_matches_reference(golden):
+    """Pinned against the reference's own smtx_read (dlcm_matrix.c:258-324, compiled into oracle/_ref): the
+    offsets and columns it returns for the committed DLMC files (tests/golden/smtx/, make_golden.py).  Values are
+    time-seeded in the reference (srand(time(NULL))), so only the structure is pinnable."""
+    d = golden("smtx_csr.npz")
+    cases = _cases(d)
+    assert len(cases) >= 4
+    for c in cases:
+        A = S.smtx_read(GOLDEN / "smtx" / f"{c}.smtx")
+        m, k = (int(v) for v in d[f"{c}.shape"])
+        assert (A.m, A.ncols, A.nnz) == (m, k, len(d[f"{c}.col_idx"])), c
+        assert np.array_equal(A.row_ptr, d[f"{c}.row_ptr"]), c
+        assert np.array_equal(A.col_idx, d[f"{c}.col_idx"]), c
+
+
+def test_smtx_reader_matches_reference_live(tmp_path):
+    """Same pin on fresh random files when oracle/_ref is built (this container only)."""
+    import oracle.oracle as O
+    if not O.ref_available("d"):
+        pytest.skip("oracle/_ref not built")
+    rng = np.random.default_rng(11)
+    for t in range(6):
+        m, n = int(rng.integers(1, 80)), int(rng.integers(1, 90))
+        deg = rng.integers(0, 12, m)
+        rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+        ci = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+        f = tmp_path / f"r{t}.smtx"
+        write_smtx(f, rp, ci, m, n)
+        rm, rk, rrp, rci = O.ref_smtx_read(str(f))
+        A = S.smtx_read(f)
+        assert (A.m, A.ncols) == (rm, rk)
+        assert np.array_equal(A.row_ptr, rrp) and np.array_equal(A.col_idx, rci)
 
 
 @pytest.mark.parametrize("text", ["3 3 2\n0 1 2 2\n0 1\n",         # header without commas
@@ -185,3 +214,45 @@ def test_bytes_alg_model():
     # 4(m+1) + (4+s) nnz + s K ncols + s K m
     assert S.bytes_alg(10, 20, 30, 4, S.F64) == 4 * 11 + 12 * 30 + 8 * 4 * 20 + 8 * 4 * 10
     assert S.bytes_alg(10, 20, 30, 4, S.F32) == 4 * 11 + 8 * 30 + 4 * 4 * 20 + 4 * 4 * 10
+
+
+def _random_dup_mtx(rng, path, m, n, nnz, col_span):
+    R = rng.integers(0, m, nnz)
+    C = rng.integers(0, col_span, nnz)
+    V = np.arange(1, nnz + 1, dtype=np.float64)          # distinct values: the order of duplicates is visible
+    with open(path, "w") as f:
+        f.write(f"%%MatrixMarket matrix coordinate real general\n{m} {n} {nnz}\n")
+        for r, c, v in zip(R, C, V):
+            f.write(f"{r + 1} {c + 1} {v}\n")
+    return R, C, V
+
+
+def test_duplicate_order_matches_reference_one_thread(tmp_path):
+    """Random COO with many duplicate (row, col) entries through both sorts of csr_sort_columns (rows longer than
+    n/5: stable bucket sort; shorter: the reference quicksort): values in the reference's order, bit for bit,
+    for the product reader and the oracle, against the reference built from its sources and run with one thread.
+    Rows are kept no longer than min(m, n): the reference's sort buffers are sized m and n (csr_gen.c:100-103)."""
+    from oracle import oracle as O
+    if not O.ref_available("d"):
+        pytest.skip("oracle/_ref not built")
+    L = O.ref_lib("d")
+    L.ref_set_threads(1)
+    rng = np.random.default_rng(0)
+    done = 0
+    for t in range(120):
+        m, n = int(rng.integers(60, 120)), int(rng.integers(2, 400))
+        nnz = int(rng.integers(0, 600))
+        span = max(1, n // int(rng.integers(1, 20)))
+        path = tmp_path / f"dup{t}.mtx"
+        R, C, V = _random_dup_mtx(rng, path, m, n, nnz, span)
+        if nnz and np.bincount(R).max() >= min(m, n):
+            continue
+        _, _, rp, ci, va = O.ref_mtx_to_csr(str(path), "d")
+        A, _, _ = S.mtx_read(path)
+        assert np.array_equal(A.row_ptr, rp) and np.array_equal(A.col_idx, ci) and np.array_equal(A.values, va), t
+        rp2, ci2, va2 = O.coo_to_csr(R, C, V, m, n)
+        assert np.array_equal(rp2, rp) and np.array_equal(ci2, ci) and np.array_equal(va2, va), t
+        B = S.coo_to_csr(R, C, V, m, n)
+        assert np.array_equal(B.values, va), t
+        done += 1
+    assert done > 80

@@ -82,7 +82,8 @@ def test_coo_to_csr_indexing_matches_reference(golden):
         m = len(rp) - 1
         R = np.repeat(np.arange(m, dtype=np.int32), np.diff(rp))
         perm = rng.permutation(len(R))
-        rp2, ci2, va2 = O.coo_to_csr(R[perm], ci[perm], va[perm], m)
+        n = int(d[f"{c}.shape"][1])
+        rp2, ci2, va2 = O.coo_to_csr(R[perm], ci[perm], va[perm], m, n)
         assert np.array_equal(rp2, rp) and np.array_equal(ci2, ci), c
 
 
