@@ -428,7 +428,7 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
 // dense column bands -- the row kernel re-gathers the same B row once per nonzero through L1/L2 (~15 TB/s chip-wide,
 // the TA/L2 request path), while the LDS reads at ~150 TB/s.  A TILE is up to RMAX consecutive C rows; the
 // inspector lists the union U of their columns (sorted) and cuts it into CHUNKS of <= UCB bytes of B rows and <=
-// CAPA entries.  Per chunk the workgroup stages (LDS-DMA) the chunk's B rows and the chunk's entries from a
+// CAPA entries.  Per chunk the workgroup stages (through VGPRs) the chunk's B rows and the chunk's entries from a
 // chunk-major copy of A: values and 16-bit byte offsets of their B rows in the staged image, row by row, each
 // row's segment padded to a multiple of 4 entries with (value +0, the all-zero B row) -- fma(+0, +0, acc) == acc
 // exactly because a chain that starts from +0 can never hold -0 -- so the inner loop reads 4 offsets and 4 values
@@ -515,10 +515,12 @@ __device__ __forceinline__ void dma_to_lds(const char *src, char *dst, int bytes
 }
 
 // Prologue: the tile's chunk descriptors and its whole union of columns land in LDS by one DMA round trip, so the
-// chunk loop never waits on a global or scalar load.  Chunk pipeline (double-buffered LDS): at the top of step c
-// the workgroup waits for chunk c's DMA (issued one step earlier) and passes a barrier (so every wave is done with
-// the buffer chunk c+1 will fill), issues chunk c+1's DMA (B rows from the LDS column list), then computes chunk c
-// while c+1 lands.
+// chunk loop never waits on a global or scalar load.  Chunk pipeline (double-buffered LDS, register staged): at the
+// top of step c a barrier makes chunk c visible to every wave and frees chunk c-1's buffer; the workgroup then
+// issues chunk c+1's global loads into VGPRs (B rows through the LDS column list; values, offsets and segment
+// offsets non-temporal), computes chunk c from LDS while they land, and writes them to the free buffer.  Register
+// staging, not LDS-DMA: a DMA in flight makes the compiler wait for lgkmcnt(0) at every LDS read of the compute
+// (measured: 0.243 vs 0.253 ms on the 39120 x 500 dense band).
 template <typename T, int VEC, int G, int RPG, int UCB, int CAPA, bool NTC, bool XCD>
 __global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict__ tiles,
                                                           const int4 *__restrict__ tchunk,
@@ -531,19 +533,19 @@ __global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict
     constexpr int NG = WG / G;
     constexpr int RMAX = NG * RPG;
     constexpr int NPL = UCB / 16 / WG;             // B pieces per lane per chunk
+    constexpr int NPV = (CAPA * (int)sizeof(T) / 16 + WG - 1) / WG;   // value pieces per lane
+    constexpr int NPO = (CAPA * 2 / 16 + WG - 1) / WG;                // offset pieces per lane
+    constexpr int NPS = ((RMAX + 8) * 2 / 16 + WG - 1) / WG;          // segment-offset pieces per lane
     constexpr int LPPR = __builtin_ctz(G);         // 16-byte pieces per staged B row == G (power of two, host)
     static_assert(UCB % (16 * WG) == 0, "UCB must be a multiple of 4 KiB");
     static_assert(VEC * sizeof(T) == 16, "16-byte lanes");
     using V = vec<T, VEC>;
     using Buf = TileBuf<T, VEC, G, UCB, CAPA, RMAX>;
     constexpr int COLMAX = tile_colmax<T, VEC, G, UCB, CAPA, RMAX>();
-    // two DISTINCT LDS objects (not an array): the compiler can then tell the chunk being read from the one the DMA
-    // is filling and does not insert a vmcnt(0) wait in front of the compute's LDS reads
     __shared__ __attribute__((aligned(16))) Buf sbuf0;
     __shared__ __attribute__((aligned(16))) Buf sbuf1;
     __shared__ __attribute__((aligned(16))) int4 sdesc[TILE_DMAX];
     __shared__ __attribute__((aligned(16))) int32_t scol[COLMAX];
-    typedef __attribute__((address_space(3))) void lds_void;
 
     const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int4 tl = tiles[b];
@@ -556,7 +558,14 @@ __global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict
     V acc[RPG];
 #pragma unroll
     for (int q = 0; q < RPG; ++q) acc[q] = vzero<T, VEC>();
-    const long long t_start = stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    // measurement stamps (stamps != nullptr): s_memtime returns through the lgkm counter out of order, so each
+    // read is waited for at once -- a pending one would make every LDS wait of the chunk loop a full drain
+    auto stamp = [&]() -> long long {
+        const long long t = (long long)__builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0)
+        return t;
+    };
+    const long long t_start = stamps ? stamp() : 0;
 
     // prologue: descriptors [tl.z, tl.z + tl.w] (the last one is the next chunk: sizes) and the union columns
     const int col0 = tchunk[tl.z].x, col1 = tchunk[tl.z + tl.w].x;
@@ -571,41 +580,69 @@ __global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict
 
     const char *Bb = reinterpret_cast<const char *>(B);
     const size_t ldb = (size_t)ld * sizeof(T);
-    auto issue = [&](int c, Buf &bf) {
+    // Every lane loads unconditionally (piece indices clamped into the chunk) and only the LDS writes are
+    // predicated: predicated loads leave partly defined registers that make the compiler wait for vmcnt(0) in
+    // front of every later load.
+    i32x4 rb[NPL], rv[NPV], ro[NPO], rs[NPS];
+    int nb = 0, nv = 0, no = 0, ns = 0;            // 16-byte pieces of the chunk in flight
+    auto load = [&](int c) {
         const int4 ch = sdesc[c], cn = sdesc[c + 1];
-        dma_to_lds((const char *)(tval + ch.z), (char *)bf.v, (cn.z - ch.z) * (int)sizeof(T), wave, wl);
-        dma_to_lds((const char *)(toff + ch.z), (char *)bf.o, (cn.z - ch.z) * 2, wave, wl);
-        dma_to_lds((const char *)(tseg + ch.w), (char *)bf.s, (cn.w - ch.w) * 2, wave, wl);
-        const int np = ch.y << LPPR;
+        nb = ch.y << LPPR;
+        nv = (cn.z - ch.z) * (int)sizeof(T) / 16;
+        no = (cn.z - ch.z) * 2 / 16;
+        ns = (cn.w - ch.w) * 2 / 16;
+        const i32x4 *gv = reinterpret_cast<const i32x4 *>(tval + ch.z);
+        const i32x4 *go = reinterpret_cast<const i32x4 *>(toff + ch.z);
+        const i32x4 *gs = reinterpret_cast<const i32x4 *>(tseg + ch.w);
 #pragma unroll
         for (int it = 0; it < NPL; ++it) {
-            const int p = it * WG + tid;
-            if (p < np) {
-                const int row = scol[ch.x - cbase + (p >> LPPR)];
-                const char *g = Bb + (size_t)row * ldb + (p & (G - 1)) * 16;
-                __builtin_amdgcn_global_load_lds((const void *)g, (lds_void *)(bf.b + it * WG + wave * 64), 16, 0, 0);
-            }
+            const int p = min(it * WG + tid, nb - 1);
+            const int row = scol[ch.x - cbase + (p >> LPPR)];
+            rb[it] = *reinterpret_cast<const i32x4 *>(Bb + (size_t)row * ldb + (p & (G - 1)) * 16);
         }
+#pragma unroll
+        for (int it = 0; it < NPV; ++it) rv[it] = __builtin_nontemporal_load(gv + min(it * WG + tid, nv - 1));
+#pragma unroll
+        for (int it = 0; it < NPO; ++it) ro[it] = __builtin_nontemporal_load(go + min(it * WG + tid, no - 1));
+#pragma unroll
+        for (int it = 0; it < NPS; ++it) rs[it] = __builtin_nontemporal_load(gs + min(it * WG + tid, ns - 1));
+    };
+    auto store = [&](Buf &bf) {
+#pragma unroll
+        for (int it = 0; it < NPL; ++it)
+            if (it * WG + tid < nb) reinterpret_cast<i32x4 *>(bf.b)[it * WG + tid] = rb[it];
+#pragma unroll
+        for (int it = 0; it < NPV; ++it)
+            if (it * WG + tid < nv) reinterpret_cast<i32x4 *>(bf.v)[it * WG + tid] = rv[it];
+#pragma unroll
+        for (int it = 0; it < NPO; ++it)
+            if (it * WG + tid < no) reinterpret_cast<i32x4 *>(bf.o)[it * WG + tid] = ro[it];
+#pragma unroll
+        for (int it = 0; it < NPS; ++it)
+            if (it * WG + tid < ns) reinterpret_cast<i32x4 *>(bf.s)[it * WG + tid] = rs[it];
     };
     long long t_wait = 0, t_comp = 0, t_mark = 0;        // measurement only (stamps != nullptr)
     auto step = [&](const Buf &cur, Buf &nxt, int c) {
-        if (stamps) t_mark = (long long)__builtin_amdgcn_s_memtime();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk c landed
-        __syncthreads();                                     // ... for every wave; chunk c-1's buffer is free
+        if (stamps) t_mark = stamp();
+        __syncthreads();                                     // chunk c visible to every wave; c-1's buffer is free
         if (stamps) {
-            const long long t = (long long)__builtin_amdgcn_s_memtime();
+            const long long t = stamp();
             t_wait += t - t_mark;
             t_mark = t;
         }
-        if (c + 1 < tl.w) issue(c + 1, nxt);
+        // the last chunk reloads itself into the free buffer (unconditional, so no load is ever left in flight
+        // on a path the compiler cannot rule out)
+        load(min(c + 1, tl.w - 1));
 #pragma unroll
         for (int q = 0; q < RPG; ++q) {
             const int r = grp + q * NG;
             if (r < tl.y) acc[q] = tile_dot<T, VEC>(acc[q], cur, lane * 16, cur.s[r] >> 2, cur.s[r + 1] >> 2);
         }
-        if (stamps) t_comp += (long long)__builtin_amdgcn_s_memtime() - t_mark;
+        store(nxt);
+        if (stamps) t_comp += stamp() - t_mark;
     };
-    issue(0, sbuf0);
+    load(0);
+    store(sbuf0);
     for (int c = 0; c < tl.w; c += 2) {
         step(sbuf0, sbuf1, c);
         if (c + 1 < tl.w) step(sbuf1, sbuf0, c + 1);
@@ -618,7 +655,7 @@ __global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict
     if (stamps && tid == 0) {
         long long *st = stamps + (size_t)b * 4;
         st[0] = t_start;
-        st[1] = (long long)__builtin_amdgcn_s_memtime();
+        st[1] = stamp();
         st[2] = t_wait;
         st[3] = t_comp;
     }
