@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""tools/pmc_dataset.py -- per-matrix HBM traffic (rocprofv3 PMC) over a stratified medium-dataset subset.
+
+BASELINE config 3 asks for "rocprof HBM-BW per matrix".  One driver process (`run`) generates each matrix of the
+subset, plans it at K (fp64), and launches `--launches` SpMMs on HBM-resident B and C; between matrices it launches a
+one-element torch fill, whose dispatch marks the boundary in the profiler's CSV.  `collect` runs that same driver
+under rocprofv3 once per counter group (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass, and
+PMC runs never carry other traces) and once with --kernel-trace for durations, then attributes every engine
+dispatch (spmm_rows_kernel / spmm_tile_kernel / spmm_combine_kernel) to its matrix by marker order.
+
+Per matrix and launch (MI355X_MICROARCH.md §HBM): read bytes = 2 x FETCH_SIZE KiB (the gfx950 wide-read correction),
+write bytes = WRITE_SIZE KiB; both sit on the L2 memory side, so Infinity-Cache hits are included (L2-miss traffic,
+an upper bound on true HBM bytes).  Rate = traffic / kernel time (sum of the launch's engine dispatches).
+
+  python tools/pmc_dataset.py collect --per-class 6 --k 32 --out profiles/r02_pmc_medium.jsonl
+"""
+import argparse
+import csv
+import json
+import subprocess
+import sys
+import time
+from collections import defaultdict
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "spmm-research_amd"))
+ENGINE = ("spmm_rows_kernel", "spmm_tile_kernel", "spmm_combine_kernel")
+PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]]
+
+
+def subset(per_class, max_nnz):
+    """per_class lines of every (avg nnz/row, bw) class, evenly spaced over the class in dataset order."""
+    from spmm_amd.datasets import medium_dataset_lines
+    cls = defaultdict(list)
+    for line in medium_dataset_lines():
+        g = line.split()
+        if int(g[0]) * float(g[2]) > max_nnz:
+            continue
+        cls[(int(g[2]), float(g[6]))].append(line)
+    out = []
+    for key in sorted(cls):
+        L = cls[key]
+        idx = np.linspace(0, len(L) - 1, per_class).round().astype(int)
+        out += [L[i] for i in sorted(set(idx))]
+    return out
+
+
+def run(args):
+    import torch
+    import spmm_amd as S
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    lines = subset(args.per_class, args.max_nnz)
+    marker = torch.zeros(1, device=dev)
+    manifest = []
+    for line in lines:
+        A = S.generate(S.gen_params(line))
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, 0, 0)
+        mf.plan(args.k)
+        g = torch.Generator(device=dev)
+        g.manual_seed(42)
+        B = torch.rand((A.ncols, args.k), generator=g, device=dev, dtype=torch.float64)
+        Cm = torch.empty((A.m, args.k), device=dev, dtype=torch.float64)
+        marker.fill_(1.0)                                   # boundary dispatch
+        for _ in range(args.launches):
+            mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), args.k, stream.cuda_stream)
+        torch.cuda.synchronize()
+        inf = mf.info()
+        manifest.append({"gen": line, "m": int(A.m), "ncols": int(A.ncols), "nnz": int(A.nnz),
+                         "bytes_alg": S.bytes_alg(A.m, A.ncols, A.nnz, args.k, S.F64), "tiles": int(inf[19]),
+                         "split_rows": int(inf[6]), "windows": int(inf[12])})
+        del mf, B, Cm
+        print(f"{len(manifest)}/{len(lines)} {line}", flush=True)
+    marker.fill_(1.0)
+    torch.cuda.synchronize()
+    Path(args.manifest).write_text(json.dumps(manifest))
+
+
+def dispatches(d):
+    """[(dispatch id, kernel name, {counter: value})] in dispatch order from a rocprofv3 output directory."""
+    rows = defaultdict(lambda: {"name": "", "c": defaultdict(float)})
+    files = list(d.rglob("*counter_collection.csv"))
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            e = rows[int(r["Dispatch_Id"])]
+            e["name"] = r["Kernel_Name"]
+            e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
+    if not files:
+        for f in d.rglob("*kernel_trace.csv"):
+            for r in csv.DictReader(open(f)):
+                e = rows[int(r["Dispatch_Id"])]
+                e["name"] = r["Kernel_Name"]
+                e["c"]["ns"] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    return [(i, rows[i]["name"], rows[i]["c"]) for i in sorted(rows)]
+
+
+def per_matrix(disp, nmat):
+    """Split the dispatch list at the marker fills (non-engine kernels between engine runs); sum per matrix."""
+    groups, cur, seen_engine = [], defaultdict(float), False
+    for _, name, c in disp:
+        if any(k in name for k in ENGINE):
+            seen_engine = True
+            for key, v in c.items():
+                cur[key] += v
+        elif "FillFunctor" in name:                       # the marker (torch fill_), not runtime memsets
+            if seen_engine:
+                groups.append(cur)
+            cur, seen_engine = defaultdict(float), False
+    if len(groups) != nmat:
+        raise SystemExit(f"dispatch groups {len(groups)} != matrices {nmat}")
+    return groups
+
+
+def collect(args):
+    outdir = ROOT / "gpurun_out" / "pmc_dataset"
+    outdir.mkdir(parents=True, exist_ok=True)
+    manifest = outdir / "manifest.json"
+    drv = [sys.executable, str(Path(__file__).resolve()), "run", "--per-class", str(args.per_class), "--k", str(args.k),
+           "--launches", str(args.launches), "--max-nnz", str(args.max_nnz), "--manifest", str(manifest)]
+    res = {}
+    for i, extra in enumerate([["--kernel-trace"]] + [["--pmc", *p] for p in PASSES]):
+        d = outdir / f"pass{i}"
+        cmd = ["rocprofv3", *extra, "--output-format", "csv", "-d", str(d), "-o", "p", "--", *drv]
+        t0 = time.time()
+        with open(outdir / f"pass{i}.log", "w") as log:
+            r = subprocess.run(cmd, stdout=log, stderr=subprocess.STDOUT, timeout=args.timeout)
+        if r.returncode != 0:
+            raise SystemExit(f"pass {i} {extra} failed rc={r.returncode} (see {outdir}/pass{i}.log)")
+        man = json.loads(manifest.read_text())
+        res[i] = per_matrix(dispatches(d), len(man))
+        print(f"pass {i} {extra[-1]}: {len(man)} matrices ({time.time() - t0:.0f}s)", flush=True)
+    with open(args.out, "w") as f:
+        for j, mrec in enumerate(man):
+            L = args.launches
+            ms = res[0][j]["ns"] / L / 1e6
+            rd = 2.0 * res[1][j]["FETCH_SIZE"] * 1024 / L
+            wr = res[2][j]["WRITE_SIZE"] * 1024 / L
+            hit, miss = res[3][j].get("TCC_HIT_sum", 0.0), res[3][j].get("TCC_MISS_sum", 0.0)
+            rec = {**mrec, "k": args.k, "dtype": "f64", "kernel_ms": ms,
+                   "gflops": 2.0 * mrec["nnz"] * args.k / (ms * 1e-3) / 1e9,
+                   "roofline_frac": mrec["bytes_alg"] / (ms * 1e-3) / 8e12,
+                   "traffic_bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                   "traffic_over_alg": (rd + wr) / mrec["bytes_alg"],
+                   "traffic_tbs": (rd + wr) / (ms * 1e-3) / 1e12,
+                   "l2_hit": hit / max(hit + miss, 1.0)}
+            f.write(json.dumps(rec) + "\n")
+    print(f"wrote {len(man)} records to {args.out}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["run", "collect"])
+    ap.add_argument("--per-class", type=int, default=6)
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--launches", type=int, default=3)
+    ap.add_argument("--max-nnz", type=float, default=4.0e7)
+    ap.add_argument("--timeout", type=int, default=500)
+    ap.add_argument("--manifest", default=str(ROOT / "gpurun_out" / "pmc_dataset" / "manifest.json"))
+    ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "pmc_dataset" / "pmc_medium.jsonl"))
+    args = ap.parse_args()
+    run(args) if args.mode == "run" else collect(args)
+
+
+if __name__ == "__main__":
+    main()
