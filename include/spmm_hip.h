@@ -81,6 +81,13 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
  * spmm_hip_run (SPMM_HIP_ASSUME_X_UNCHANGED). */
 int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *d_c, int32_t k, void *stream);
 
+/* Independent SpMMs of `count` DIFFERENT handles (e.g. the pipeline's K/Q/V projections), run concurrently: the
+ * first on `stream`, the others on side streams of this device forked from and joined back into `stream` by events
+ * (graph-capturable: a capture on `stream` takes the side streams along).  Same arguments per entry as
+ * spmm_hip_run_device; every entry computes exactly what spmm_hip_run_device would. */
+int spmm_hip_run_device_batch(int32_t count, spmm_hip_t *const *h, const void *const *d_b, const int32_t *b_layout,
+                              void *const *d_c, const int32_t *k, void *stream);
+
 /* Execute, host buffers with B ROW-major (x[col*k + n]; the layout the reference pipeline plugin hands MKL's csrmm,
  * pipeline_code_bench/sddmm_taco_naive.cpp:219-249): uploads x into the engine's B directly (no transpose), runs,
  * downloads y (row-major [m][k]).  Synchronous. */

@@ -65,15 +65,46 @@ __device__ __forceinline__ double fma_t(double a, double b, double c) { return _
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // ROWDIAG: s[i] = fma chain over t of Q[i][t] * K[i][t] from 0 (compute2's inner loop for any nonzero of row i).
+// One lane per row keeps the chain serial (bit-identical).  A one-wave workgroup owns RD_ROWS consecutive rows: the
+// wave first stages their Q and K rows (up to RD_T elements at a time) in LDS by LDS-DMA -- every instruction moves
+// 256 consecutive bytes of one row, all in flight before one wait -- then lanes 0..RD_ROWS-1 run their chains from LDS
+// (row pitch RD_T+1: conflict-free).  Few rows per workgroup spread the m chains over many CUs.  The direct form,
+// lane i reading Q[i][t] from HBM, touched 64 lines per load instruction (124 us at m = n = 512; this form, DESIGN
+// §6.10).
+constexpr int RD_ROWS = 16, RD_T = 512, RD_WG = 64;
 template <typename T>
-__global__ __launch_bounds__(WG) void rowdiag_chain_kernel(const T *__restrict__ Q, const T *__restrict__ K,
-                                                           T *__restrict__ s, int64_t m, int n) {
-    const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
-    if (i >= m) return;
-    const T *q = Q + i * n, *k = K + i * n;
+__global__ __launch_bounds__(RD_WG) void rowdiag_chain_kernel(const T *__restrict__ Q, const T *__restrict__ K,
+                                                              T *__restrict__ s, int64_t m, int n) {
+    __shared__ T sq[RD_ROWS][RD_T + 1], sk[RD_ROWS][RD_T + 1];
+    const int l = threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.x * RD_ROWS;
+    const int rows = (int)std::min<int64_t>(RD_ROWS, m - i0);
     T acc = T(0);
-    for (int t = 0; t < n; ++t) acc = fma_t(q[t], k[t], acc);
-    s[i] = acc;
+    typedef __attribute__((address_space(3))) void lds_void;
+    for (int t0 = 0; t0 < n; t0 += RD_T) {
+        const int tn = std::min(RD_T, n - t0);
+        const int dw = tn * (int)sizeof(T) / 4;               // dwords of one row piece
+        // LDS-DMA, 64 dwords (one 256-B row segment) per instruction, all issued before the one wait
+        for (int r = 0; r < rows; ++r) {
+            const char *q = reinterpret_cast<const char *>(Q + (i0 + r) * n + t0);
+            const char *k = reinterpret_cast<const char *>(K + (i0 + r) * n + t0);
+            for (int c = 0; c < dw; c += RD_WG)
+                if (c + l < dw) {
+                    __builtin_amdgcn_global_load_lds((const void *)(q + (c + l) * 4),
+                                                     (lds_void *)(reinterpret_cast<char *>(&sq[r][0]) + c * 4), 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void *)(k + (c + l) * 4),
+                                                     (lds_void *)(reinterpret_cast<char *>(&sk[r][0]) + c * 4), 4, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (l < rows) {
+#pragma unroll 8
+            for (int t = 0; t < tn; ++t) acc = fma_t(sq[l][t], sk[l][t], acc);
+        }
+        __syncthreads();
+    }
+    if (l < rows) s[i0 + l] = acc;
 }
 
 // y[p] = s[row(p)] * a[p]  (compute2's `B[pA2] *= A_vals[pA2]` after the chain)
@@ -158,7 +189,7 @@ int run_t(spmm_sddmm_t *s, const T *Q, const T *K, T *y, hipStream_t st) {
     if (nnz == 0) return SPMM_HIP_OK;
     const unsigned gp = (unsigned)((nnz + WG - 1) / WG);
     if ((s->flags & 1) == SPMM_SDDMM_REF_ROWDIAG) {
-        rowdiag_chain_kernel<T><<<(unsigned)((m + WG - 1) / WG), WG, 0, st>>>(Q, K, (T *)s->d_s, m, s->n);
+        rowdiag_chain_kernel<T><<<(unsigned)((m + RD_ROWS - 1) / RD_ROWS), RD_WG, 0, st>>>(Q, K, (T *)s->d_s, m, s->n);
         rowdiag_scale_kernel<T><<<gp, WG, 0, st>>>((const T *)s->d_s, s->d_prow, (const T *)s->d_a, y, nnz);
     } else {
         // K [ncols][n] -> KT [n][ncols]: the engine's tile transpose (it maps X[r*ncols + c] -> Bt[c*R + r])

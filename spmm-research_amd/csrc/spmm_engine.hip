@@ -24,6 +24,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -56,7 +58,7 @@ constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may
 constexpr int TILE_UCB = 12 * 1024;       // LDS bytes of staged B rows per chunk (two chunk buffers per workgroup)
 constexpr int TILE_CAPA = 896;            // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
 constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
-constexpr double TILE_MIN_REUSE = 12.0;   // policy: sampled reuse (nnz per union column) to leave the row kernel
+constexpr double TILE_MIN_REUSE = 8.0;    // policy: sampled reuse (nnz per union column) to leave the row kernel (§6.9)
                                           // (measured, DESIGN §6.9: 1.22x at ~14 on 39 K x 500 bw 0.05; 0.66-0.82x
                                           // at 4.5-6; the kernel is LDS-throughput bound)
 constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
@@ -1413,6 +1415,64 @@ int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *
     if (ev) HIPCHK(hipEventRecord(h->ev[1], s));
     h->have_times = ev;
     h->have_copies = false;
+    return SPMM_HIP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// Side streams and fork/join events of spmm_hip_run_device_batch, per device, created on first use and kept.
+struct BatchPool {
+    std::vector<hipStream_t> side;
+    std::vector<hipEvent_t> join;
+    hipEvent_t fork = nullptr;
+};
+std::mutex g_batch_mu;
+std::map<int, BatchPool> g_batch_pools;
+}  // namespace
+
+extern "C" {
+
+int spmm_hip_run_device_batch(int32_t count, spmm_hip_t *const *hs, const void *const *d_b, const int32_t *b_layout,
+                              void *const *d_c, const int32_t *k, void *stream) {
+    if (count < 1 || !hs || !d_b || !b_layout || !d_c || !k) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: bad arguments");
+    for (int i = 0; i < count; ++i) {
+        if (!hs[i]) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: null handle");
+        if (hs[i]->device != hs[0]->device) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: handles on different devices");
+        for (int j = 0; j < i; ++j)
+            if (hs[j] == hs[i]) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: a handle appears twice");
+    }
+    if (count == 1) return spmm_hip_run_device(hs[0], d_b[0], b_layout[0], d_c[0], k[0], stream);
+    // plan (host work, may allocate) before the fork, so nothing below allocates inside a graph capture
+    for (int i = 0; i < count; ++i)
+        if (hs[i]->plan.k != k[i]) {
+            int st = spmm_hip_plan(hs[i], k[i]);
+            if (st != SPMM_HIP_OK) return st;
+        }
+    std::lock_guard<std::mutex> lock(g_batch_mu);
+    const int dev = hs[0]->device;
+    HIPCHK(hipSetDevice(dev));
+    BatchPool &pool = g_batch_pools[dev];
+    if (!pool.fork) HIPCHK(hipEventCreateWithFlags(&pool.fork, hipEventDisableTiming));
+    while ((int)pool.side.size() < count - 1) {
+        hipStream_t st;
+        hipEvent_t ev;
+        HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        pool.side.push_back(st);
+        pool.join.push_back(ev);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipEventRecord(pool.fork, s));
+    for (int i = 1; i < count; ++i) {
+        HIPCHK(hipStreamWaitEvent(pool.side[i - 1], pool.fork, 0));
+        int st = spmm_hip_run_device(hs[i], d_b[i], b_layout[i], d_c[i], k[i], pool.side[i - 1]);
+        if (st != SPMM_HIP_OK) return st;
+        HIPCHK(hipEventRecord(pool.join[i - 1], pool.side[i - 1]));
+    }
+    int st = spmm_hip_run_device(hs[0], d_b[0], b_layout[0], d_c[0], k[0], s);
+    if (st != SPMM_HIP_OK) return st;
+    for (int i = 1; i < count; ++i) HIPCHK(hipStreamWaitEvent(s, pool.join[i - 1], 0));
     return SPMM_HIP_OK;
 }
 

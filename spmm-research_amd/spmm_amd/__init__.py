@@ -105,6 +105,8 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)]
     L.spmm_hip_run.argtypes = [vp, vp, vp, i32]
     L.spmm_hip_run_device.argtypes = [vp, vp, i32, vp, i32, vp]
+    L.spmm_hip_run_device_batch.argtypes = [i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32), C.POINTER(vp),
+                                            C.POINTER(i32), vp]
     L.spmm_hip_plan.argtypes = [vp, i32]
     L.spmm_hip_last_times.argtypes = [vp, _f64p]
     L.spmm_hip_set_timing.argtypes = [vp, i32]
@@ -481,6 +483,19 @@ class MatrixFormat:
             self.close()
         except Exception:
             pass
+
+
+def run_device_batch(entries, stream: int = 0) -> None:
+    """Independent HBM-resident SpMMs of different handles, run concurrently (spmm_hip_run_device_batch): entries =
+    [(MatrixFormat, d_b, b_layout, d_c, k), ...]; the first runs on `stream`, the rest on forked side streams joined
+    back into it (graph-capturable)."""
+    n = len(entries)
+    hs = (C.c_void_p * n)(*[e[0]._h for e in entries])
+    bs = (C.c_void_p * n)(*[e[1] for e in entries])
+    lay = (C.c_int32 * n)(*[e[2] for e in entries])
+    cs = (C.c_void_p * n)(*[e[3] for e in entries])
+    ks = (C.c_int32 * n)(*[e[4] for e in entries])
+    _check("run_device_batch", hip.spmm_hip_run_device_batch(n, hs, bs, lay, cs, ks, C.c_void_p(stream)))
 
 
 def csr_to_format(row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0) -> MatrixFormat:

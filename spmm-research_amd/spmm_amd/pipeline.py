@@ -24,7 +24,7 @@ import ctypes as C
 
 import numpy as np
 
-from . import CSR, F32, F64, B_ROW_MAJOR, SpmmHipError, csr_to_format, hip
+from . import CSR, F32, F64, B_ROW_MAJOR, SpmmHipError, csr_to_format, hip, run_device_batch
 
 SDDMM_REF_ROWDIAG, SDDMM_QKT, SDDMM_SOFTMAX = 0, 1, 2
 
@@ -132,8 +132,9 @@ class SparseAttentionPipeline:
 
     def run_device(self, d_x: int, d_k: int, d_q: int, d_v: int, d_y: int, d_out: int, stream: int = 0) -> None:
         """One pipeline step on device buffers (row-major): x [k][n] -> K, Q, V [m][n], y [mask nnz], out [m][n]."""
-        for t, d in (("K", d_k), ("Q", d_q), ("V", d_v)):
-            self.mf[t].spmm_device(d_x, B_ROW_MAJOR, d, self.n, stream)
+        # the three projections are independent: one concurrent batch (side streams forked from `stream`)
+        run_device_batch([(self.mf[t], d_x, B_ROW_MAJOR, d, self.n) for t, d in (("K", d_k), ("Q", d_q), ("V", d_v))],
+                         stream)
         self.sddmm.run_device(d_q, d_k, d_y, stream)
         self.final.update_values_device(d_y, stream)
         self.final.spmm_device(d_v, B_ROW_MAJOR, d_out, self.n, stream)

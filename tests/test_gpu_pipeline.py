@@ -191,3 +191,48 @@ def test_reference_plugin_pipeline(env, tmp_path, vt, dtype, mode):
         assert np.array_equal(bits(got), bits(want.ravel()))
     yf = O.spmm_rowmajor(mask.row_ptr, mask.col_idx, parts[3], mask.ncols, parts[2].reshape(-1, n))
     assert np.array_equal(bits(parts[4]), bits(yf.ravel()))
+
+
+def test_run_device_batch_equals_sequential(env, monkeypatch):
+    """spmm_hip_run_device_batch (independent handles on forked side streams) == one spmm_hip_run_device per handle,
+    bit for bit, eagerly and replayed from a captured hipGraph; split rows allowed (default inspector)."""
+    torch, S, P, O = env
+    monkeypatch.delenv("SPMM_HIP_SEQ_MAX")
+    monkeypatch.delenv("SPMM_HIP_LANES")
+    dev = torch.device("cuda", 0)
+    mats = [S.generate(S.gen_params(l)) for l in ("3000 2000 40 30 normal random 0.3 1000 0.5 0.5 14",
+                                                  "5000 2000 8 2 normal random 0.05 0 0.5 0.95 14",
+                                                  "700 2000 300 100 normal random 0.6 10 0.5 0.5 14")]
+    k = 48
+    mfs = [S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0) for A in mats]
+    B = torch.rand((2000, k), dtype=torch.float64, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    Bt = B.t().contiguous()                                   # the same B column-major for the second entry
+    lay = [S.B_ROW_MAJOR, S.B_COL_MAJOR, S.B_ROW_MAJOR]
+    bsrc = [B, Bt, B]
+    want, got = [], []
+    s = torch.cuda.Stream(dev)
+    for mf, A, b, L in zip(mfs, mats, bsrc, lay):
+        c = torch.empty((A.m, k), dtype=torch.float64, device=dev)
+        with torch.cuda.stream(s):
+            mf.spmm_device(b.data_ptr(), L, c.data_ptr(), k, s.cuda_stream)
+        want.append(c)
+        got.append(torch.full((A.m, k), float("nan"), dtype=torch.float64, device=dev))
+    entries = [(mf, b.data_ptr(), L, c.data_ptr(), k) for mf, b, L, c in zip(mfs, bsrc, lay, got)]
+    with torch.cuda.stream(s):
+        S.run_device_batch(entries, s.cuda_stream)
+    torch.cuda.synchronize()
+    for w, g in zip(want, got):
+        assert np.array_equal(bits(w.cpu().numpy()), bits(g.cpu().numpy()))
+    for g in got:
+        g.fill_(float("nan"))
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        S.run_device_batch(entries, s.cuda_stream)
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    for w, g in zip(want, got):
+        assert np.array_equal(bits(w.cpu().numpy()), bits(g.cpu().numpy()))
+    for mf in mfs:
+        mf.close()
