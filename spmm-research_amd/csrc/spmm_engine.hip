@@ -59,6 +59,8 @@ constexpr int TILE_UCB = 12 * 1024;       // LDS bytes of staged B rows per chun
 constexpr int TILE_CAPA = 896;            // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
 constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
 constexpr double TILE_MIN_REUSE = 8.0;    // policy: sampled reuse (nnz per union column) to leave the row kernel (§6.9)
+constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgroup each) to fill 256 CUs twice (§6.9:
+                                          // 76-173 tiles ran 2.7-3x slower than the row kernel's split rows)
                                           // (measured, DESIGN §6.9: 1.22x at ~14 on 39 K x 500 bw 0.05; 0.66-0.82x
                                           // at 4.5-6; the kernel is LDS-throughput bound)
 constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
@@ -1148,7 +1150,8 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                 const char *thr = getenv("SPMM_HIP_TILE_REUSE");
                 const double min_reuse = forced > 0 ? 1.0 : (thr && *thr) ? atof(thr) : TILE_MIN_REUSE;
                 pl.tile_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax);
-                if (forced > 0 || pl.tile_reuse >= min_reuse)
+                const bool enough = (h->m + rmax - 1) / rmax >= TILE_MIN_TILES;
+                if (forced > 0 || (enough && pl.tile_reuse >= min_reuse))
                     tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax,
                                         (int)(TILE_UCB / srow), TILE_CAPA, min_reuse, tp,
                                         tile_colmax_for(h->vsize, g_t) - 4, TILE_DMAX - 1);
