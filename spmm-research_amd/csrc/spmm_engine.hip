@@ -55,8 +55,14 @@ int fail(int status, const std::string &what) {
 constexpr int CAP = 2048;         // LDS capacity of a block (nonzeros)
 constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may read up to 3 elements past nnz)
 // LDS B tiles (spmm_tile_kernel)
-constexpr int TILE_UCB = 12 * 1024;       // LDS bytes of staged B rows per chunk (two chunk buffers per workgroup)
-constexpr int TILE_CAPA = 896;            // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
+#ifndef SPMM_TILE_UCB_KB
+#define SPMM_TILE_UCB_KB 12                // A/B builds only
+#endif
+#ifndef SPMM_TILE_CAPA
+#define SPMM_TILE_CAPA 896
+#endif
+constexpr int TILE_UCB = SPMM_TILE_UCB_KB * 1024;   // LDS bytes of staged B rows per chunk (two chunk buffers per workgroup)
+constexpr int TILE_CAPA = SPMM_TILE_CAPA;           // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
 constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
 constexpr double TILE_MIN_REUSE = 8.0;    // policy: sampled reuse (nnz per union column) to leave the row kernel (§6.9)
 constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgroup each) to fill 256 CUs twice (§6.9:

@@ -443,7 +443,11 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
 // LDS budget of one tile workgroup (3 per CU: 3 x 53,248 B with the 512-B allocation granule).
-constexpr int TILE_LDS_BYTES = 53248;
+#ifndef SPMM_TILE_WGS
+#define SPMM_TILE_WGS 3                        // A/B builds only: tile workgroups per CU (LDS budget and launch bounds)
+#endif
+constexpr int TILE_WGS = SPMM_TILE_WGS;
+constexpr int TILE_LDS_BYTES = TILE_WGS == 3 ? 53248 : TILE_WGS == 4 ? 40448 : 79872;
 constexpr int TILE_DMAX = 64;                  // chunk descriptors per tile (incl. the end marker)
 
 template <typename T, int VEC, int G, int UCB, int CAPA, int RMAX>
@@ -522,7 +526,7 @@ __device__ __forceinline__ void dma_to_lds(const char *src, char *dst, int bytes
 // staging, not LDS-DMA: a DMA in flight makes the compiler wait for lgkmcnt(0) at every LDS read of the compute
 // (measured: 0.243 vs 0.253 ms on the 39120 x 500 dense band).
 template <typename T, int VEC, int G, int RPG, int UCB, int CAPA, bool NTC, bool XCD>
-__global__ __launch_bounds__(WG, 3) void spmm_tile_kernel(const int4 *__restrict__ tiles,
+__global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__restrict__ tiles,
                                                           const int4 *__restrict__ tchunk,
                                                           const int32_t *__restrict__ tcol,
                                                           const uint16_t *__restrict__ tseg,
