@@ -150,3 +150,29 @@ def test_tiles_graph_replay(env, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(C1.view(torch.int64), C2.view(torch.int64))
     mf.close()
+
+
+def test_tile_policy_gates(env, monkeypatch):
+    """The default policy: tiles need sampled reuse >= 8 AND >= 512 candidate tiles.  A small dense
+    matrix (2,445 rows, 77 candidate tiles) stays with the row kernel even though its reuse is high; a large
+    high-reuse band takes tiles; both stay exact where the engine says so."""
+    torch, S, O = env
+    monkeypatch.delenv("SPMM_HIP_TILES", raising=False)
+    k = 32
+    for line, want in (("2445 2445 500 166.6667 normal random 0.05 10000 0.95 0.95 14", False),
+                       ("22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14", True)):
+        A = S.generate(S.gen_params(line))
+        x = np.random.default_rng(1).uniform(0, 1, A.ncols * k)          # the reference's column-major x
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0)
+        y = np.full(A.m * k, np.nan)
+        mf.spmm(x, y, k)
+        ti, ex = mf.tile_info(), mf.exact_rows()
+        mf.close()
+        assert (ti["tiles"] > 0) == want, (line, ti)
+        rows = np.random.default_rng(2).choice(A.m, 300, replace=False)
+        sub = S.CSR(np.concatenate([[0], np.cumsum(np.diff(A.row_ptr)[rows])]).astype(np.int32),
+                    np.concatenate([A.col_idx[A.row_ptr[r]:A.row_ptr[r + 1]] for r in rows]),
+                    np.concatenate([A.values[A.row_ptr[r]:A.row_ptr[r + 1]] for r in rows]), len(rows), A.ncols)
+        ys = y.reshape(A.m, k)[rows]
+        seq = O.spmm(sub.row_ptr, sub.col_idx, sub.values, A.ncols, x, k)
+        assert np.array_equal(bits(ys[ex[rows]]), bits(seq[ex[rows]]))
