@@ -77,7 +77,8 @@ def main():
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "spmm-research_amd"))
     import bench  # for the workload defaults and the engine fingerprint
-    gen = args.gen or bench.GEN_LINE
+    from spmm_amd.datasets import CONFIG2_LINE
+    gen = args.gen or CONFIG2_LINE
     fetch_kib = res.get("FETCH_SIZE", {}).get("mean")
     write_kib = res.get("WRITE_SIZE", {}).get("mean")
     hbm = None
