@@ -408,7 +408,10 @@ int split_length(const spmm_hip_t *h, int kw) {
     const double est_us = 1.3 * ((double)h->nnz * kw * s / 12.0e6 +
                                  ((double)h->nnz * (4.0 + s) + (double)h->m * kw * s + 4.0 * h->m) / 6.0e6) + 10.0;
     double t = CHAIN_NNZ_PER_US * est_us * (double)h->var.u / 16.0;
-    if (h->m >= 2048) t = std::max(t, 2.5 * (double)h->nnz / (double)std::max<int64_t>(h->m, 1));
+    // rows at least 2.5x the mean stay whole: splitting every row of a small long-row matrix (698 x 500) is 1.4-4.7x
+    // slower than whole rows with vector lanes (profiles/r02_small_split.jsonl)
+    const double mean = (double)h->nnz / (double)std::max<int64_t>(h->m, 1);
+    if (h->m >= 2048 || mean >= 32.0) t = std::max(t, 2.5 * mean);
     return (int)std::max(64.0, std::min((double)CAP, t));
 }
 
