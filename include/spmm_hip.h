@@ -83,8 +83,9 @@ int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *
 
 /* Independent SpMMs of `count` DIFFERENT handles (e.g. the pipeline's K/Q/V projections), run concurrently: the
  * first on `stream`, the others on side streams of this device forked from and joined back into `stream` by events
- * (graph-capturable: a capture on `stream` takes the side streams along).  Same arguments per entry as
- * spmm_hip_run_device; every entry computes exactly what spmm_hip_run_device would. */
+ * (graph-capturable: a capture on `stream` takes the side streams along; the first call on a device creates its
+ * side streams and events, so make it before capturing, like the planning run of each handle).  Same arguments per
+ * entry as spmm_hip_run_device; every entry computes exactly what spmm_hip_run_device would. */
 int spmm_hip_run_device_batch(int32_t count, spmm_hip_t *const *h, const void *const *d_b, const int32_t *b_layout,
                               void *const *d_c, const int32_t *k, void *stream);
 
