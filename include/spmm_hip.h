@@ -146,9 +146,10 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
 
 /* LDS B tiles of the current plan: runs of up to 64 consecutive rows whose union of columns is
  * read several times (similar or dense rows) are computed by a second kernel that stages each B row of the union
- * in LDS once; every tile row is still one left-to-right FMA chain in CSR order (exact).  out has 6 slots:
+ * in LDS once; every tile row is still one left-to-right FMA chain in CSR order (exact).  out has 7 slots:
  * out[0]=tiles, out[1]=rows in tiles, out[2]=nonzeros in tiles, out[3]=chunks (LDS fills), out[4]=the sampled
- * mean reuse (nonzeros per union column) x 1000 the policy decided on, out[5]=1 when tiles run in XCD order.
+ * mean reuse (nonzeros per union column) x 1000 the policy decided on, out[5]=1 when tiles run in XCD order,
+ * out[6]=1 when tiles use 32-byte compute lanes (SPMM_HIP_TILE_WIDE).
  * SPMM_HIP_TILES=-1 disables tiles, =1 takes every eligible tile; SPMM_HIP_TILE_REUSE=<x> sets the threshold. */
 int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out);
 

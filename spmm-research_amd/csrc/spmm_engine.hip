@@ -63,6 +63,7 @@ constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may
 #endif
 constexpr int TILE_UCB = SPMM_TILE_UCB_KB * 1024;   // LDS bytes of staged B rows per chunk (two chunk buffers per workgroup)
 constexpr int TILE_CAPA = SPMM_TILE_CAPA;           // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
+constexpr int TILE_WIDE_DEFAULT = 0;      // SPMM_HIP_TILE_WIDE: 32-byte compute lanes in tile mode
 constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
 constexpr double TILE_MIN_REUSE = 8.0;    // policy: sampled reuse (nnz per union column) to leave the row kernel (§6.9)
 constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgroup each) to fill 256 CUs twice (§6.9:
@@ -101,6 +102,7 @@ struct Plan {
     int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
     int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
     int tile_xcd = 0;          // tiles in XCD-contiguous order
+    int tile_wide = 0;         // 32-byte compute lanes (two 16-byte pieces of a B row per lane), where RPG allows
     int64_t tile_rows = 0, tile_nnz = 0, tile_chunks = 0;
     double tile_reuse = 0.0;   // sampled mean reuse (nnz per union column) the policy saw
 };
@@ -337,12 +339,19 @@ void launch_tiles_g(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t
     constexpr int VEC = 16 / (int)sizeof(T);
     constexpr int NG = WG / G;
     constexpr int RPG = NG * 8 <= TILE_RMAX ? 8 : (TILE_RMAX / NG > 1 ? TILE_RMAX / NG : 1);
-    auto go = [&](auto xcd_c) {
-        spmm_tile_kernel<T, VEC, G, RPG, TILE_UCB, TILE_CAPA, (bool)DEF_NTC, decltype(xcd_c)::value>
+    auto go = [&](auto xcd_c, auto s_c) {
+        constexpr int SW = decltype(s_c)::value;
+        spmm_tile_kernel<T, VEC, G, RPG / SW, TILE_UCB, TILE_CAPA, (bool)DEF_NTC, decltype(xcd_c)::value, SW>
             <<<h->plan.ntile, WG, 0, s>>>(h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg, (const T *)h->d_tval,
                                            h->d_tlidx, B, C, ld, h->d_tstamps);
     };
-    if (h->plan.tile_xcd) go(std::true_type()); else go(std::false_type());
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, (RPG % 2 == 0 && G >= 2) ? 2 : 1>;
+    if (h->plan.tile_wide) {
+        if (h->plan.tile_xcd) go(std::true_type(), S2()); else go(std::false_type(), S2());
+    } else {
+        if (h->plan.tile_xcd) go(std::true_type(), S1()); else go(std::false_type(), S1());
+    }
 }
 
 template <typename T>
@@ -1174,6 +1183,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             // consecutive tiles share most of their columns: in XCD order they share an L2 as well
             const int env_x = env_int("SPMM_HIP_TILE_XCD", 1);
             pl.tile_xcd = (env_x > 0 && pl.ntile >= 64) ? 1 : 0;
+            pl.tile_wide = (env_int("SPMM_HIP_TILE_WIDE", TILE_WIDE_DEFAULT) > 0 && tile_rpg(g_t) % 2 == 0) ? 1 : 0;
         }
     }
 
@@ -1694,6 +1704,7 @@ int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out) {
     out[3] = h->plan.tile_chunks;
     out[4] = (int64_t)(h->plan.tile_reuse * 1000.0 + 0.5);
     out[5] = h->plan.tile_xcd;
+    out[6] = h->plan.tile_wide;
     return SPMM_HIP_OK;
 }
 

@@ -469,7 +469,7 @@ constexpr int tile_colmax() {
 template <typename T, int VEC, typename Buf>
 __device__ __forceinline__ void tile_step(vec<T, VEC> &acc, const char *bb, int bl, const u16x4 o,
                                           const vec<T, 4> &av) {
-    using V = vec<T, VEC>;
+    using V = vec<T, VEC>;             // VEC = the lane's values of one B row (16 or 32 bytes)
     const V b0 = *reinterpret_cast<const V *>(bb + (bl + (int)o.x));
     const V b1 = *reinterpret_cast<const V *>(bb + (bl + (int)o.y));
     const V b2 = *reinterpret_cast<const V *>(bb + (bl + (int)o.z));
@@ -525,7 +525,11 @@ __device__ __forceinline__ void dma_to_lds(const char *src, char *dst, int bytes
 // offsets non-temporal), computes chunk c from LDS while they land, and writes them to the free buffer.  Register
 // staging, not LDS-DMA: a DMA in flight makes the compiler wait for lgkmcnt(0) at every LDS read of the compute
 // (measured: 0.243 vs 0.253 ms on the 39120 x 500 dense band).
-template <typename T, int VEC, int G, int RPG, int UCB, int CAPA, bool NTC, bool XCD>
+//
+// S = 16-byte pieces of a B row per compute lane (1, or 2 = "wide" lanes): G/S lanes per row group and RPG rows per
+// group (the host passes RPG / S, so the tile geometry NG x RPG -- and with it the inspector's layout -- is the same);
+// wide lanes halve the broadcast reads of values and offsets per FMA.  Staging always moves 16-byte pieces.
+template <typename T, int VEC, int G, int RPG, int UCB, int CAPA, bool NTC, bool XCD, int S = 1>
 __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__restrict__ tiles,
                                                           const int4 *__restrict__ tchunk,
                                                           const int32_t *__restrict__ tcol,
@@ -534,8 +538,11 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
                                                           const uint16_t *__restrict__ toff,
                                                           const T *__restrict__ B, T *__restrict__ C, int ld,
                                                           long long *__restrict__ stamps) {
-    constexpr int NG = WG / G;
+    constexpr int GC = G / S;                      // compute lanes per row group
+    constexpr int NG = WG / GC;
     constexpr int RMAX = NG * RPG;
+    static_assert(S == 1 || S == 2, "16- or 32-byte compute lanes");
+    static_assert(GC >= 1 && G % S == 0, "lanes");
     constexpr int NPL = UCB / 16 / WG;             // B pieces per lane per chunk
     constexpr int NPV = (CAPA * (int)sizeof(T) / 16 + WG - 1) / WG;   // value pieces per lane
     constexpr int NPO = (CAPA * 2 / 16 + WG - 1) / WG;                // offset pieces per lane
@@ -543,7 +550,7 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
     constexpr int LPPR = __builtin_ctz(G);         // 16-byte pieces per staged B row == G (power of two, host)
     static_assert(UCB % (16 * WG) == 0, "UCB must be a multiple of 4 KiB");
     static_assert(VEC * sizeof(T) == 16, "16-byte lanes");
-    using V = vec<T, VEC>;
+    using VW = vec<T, VEC * S>;                    // a compute lane's slice of a B / C row
     using Buf = TileBuf<T, VEC, G, UCB, CAPA, RMAX>;
     constexpr int COLMAX = tile_colmax<T, VEC, G, UCB, CAPA, RMAX>();
     __shared__ __attribute__((aligned(16))) Buf sbuf0;
@@ -554,14 +561,14 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
     const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int4 tl = tiles[b];
     const int tid = threadIdx.x, wave = tid / 64, wl = tid % 64;
-    const int grp = tid / G, lane = tid % G;
+    const int grp = tid / GC, lane = tid % GC;
     if (tid < G) {
         sbuf0.b[UCB / 16 + tid] = vzero<T, VEC>();
         sbuf1.b[UCB / 16 + tid] = vzero<T, VEC>();
     }
-    V acc[RPG];
+    VW acc[RPG];
 #pragma unroll
-    for (int q = 0; q < RPG; ++q) acc[q] = vzero<T, VEC>();
+    for (int q = 0; q < RPG; ++q) acc[q] = vzero<T, VEC * S>();
     // measurement stamps (stamps != nullptr): s_memtime returns through the lgkm counter out of order, so each
     // read is waited for at once -- a pending one would make every LDS wait of the chunk loop a full drain
     auto stamp = [&]() -> long long {
@@ -640,7 +647,7 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
 #pragma unroll
         for (int q = 0; q < RPG; ++q) {
             const int r = grp + q * NG;
-            if (r < tl.y) acc[q] = tile_dot<T, VEC>(acc[q], cur, lane * 16, cur.s[r] >> 2, cur.s[r + 1] >> 2);
+            if (r < tl.y) acc[q] = tile_dot<T, VEC * S>(acc[q], cur, lane * 16 * S, cur.s[r] >> 2, cur.s[r + 1] >> 2);
         }
         store(nxt);
         if (stamps) t_comp += stamp() - t_mark;
@@ -654,7 +661,7 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
 #pragma unroll
     for (int q = 0; q < RPG; ++q) {
         const int r = grp + q * NG;
-        if (r < tl.y) vstore<T, VEC, NTC>(C + (size_t)(tl.x + r) * ld + lane * VEC, acc[q]);
+        if (r < tl.y) vstore<T, VEC * S, NTC>(C + (size_t)(tl.x + r) * ld + lane * VEC * S, acc[q]);
     }
     if (stamps && tid == 0) {
         long long *st = stamps + (size_t)b * 4;

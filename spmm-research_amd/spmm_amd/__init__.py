@@ -446,10 +446,10 @@ class MatrixFormat:
 
     def tile_info(self) -> dict:
         """LDS B tiles of the current plan (spmm_hip_tile_info)."""
-        out = np.zeros(6, np.int64)
+        out = np.zeros(7, np.int64)
         _check("tile_info", hip.spmm_hip_tile_info(self._h, out))
         return {"tiles": int(out[0]), "rows": int(out[1]), "nnz": int(out[2]), "chunks": int(out[3]),
-                "reuse": out[4] / 1000.0, "xcd": int(out[5])}
+                "reuse": out[4] / 1000.0, "xcd": int(out[5]), "wide": int(out[6])}
 
     def exact_rows(self) -> np.ndarray:
         """bool[m]: rows computed as the reference's single left-to-right FMA chain (bit-identical to it)."""

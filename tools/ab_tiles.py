@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--lines", default="", help="';'-separated generator lines (default: a built-in set)")
     ap.add_argument("--k", default="32")
     ap.add_argument("--dtype", default="f64")
-    ap.add_argument("--modes", default="-1,0,1")
+    ap.add_argument("--modes", default="-1,0,1",
+                    help="SPMM_HIP_TILES values; a 'w' suffix (e.g. 1w) adds SPMM_HIP_TILE_WIDE=1, others get =0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--env", default="", help="extra KEY=VAL;KEY=VAL for the tile handles")
@@ -42,7 +43,7 @@ def main():
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     lines = args.lines.split(";") if args.lines else LINES
-    modes = [int(x) for x in args.modes.split(",")]
+    modes = args.modes.split(",")
     extra = dict(kv.split("=", 1) for kv in args.env.split(";") if kv)
     for line in lines:
         A = S.generate(S.gen_params(line))
@@ -53,14 +54,16 @@ def main():
                 vals = A.values.astype(npdt)
                 hs = {}
                 for md in modes:
-                    os.environ["SPMM_HIP_TILES"] = str(md)
+                    os.environ["SPMM_HIP_TILES"] = md.rstrip("w")
+                    os.environ["SPMM_HIP_TILE_WIDE"] = "1" if md.endswith("w") else "0"
                     for kk, vv in extra.items():
-                        if md >= 0:
+                        if int(md.rstrip("w")) >= 0:
                             os.environ[kk] = vv
                         else:
                             os.environ.pop(kk, None)
                     hs[md] = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, k, 0)
                 os.environ.pop("SPMM_HIP_TILES", None)
+                os.environ.pop("SPMM_HIP_TILE_WIDE", None)
                 for kk in extra:
                     os.environ.pop(kk, None)
                 g = torch.Generator(device=dev)
@@ -96,7 +99,7 @@ def main():
                     out[str(md)] = {"ms": round(med, 5), "gflops": round(2.0 * A.nnz * k / med / 1e6, 1),
                                     "frac": round(b / (med * 1e-3) / 8e12, 4), "tiles": ti["tiles"],
                                     "tile_rows": ti["rows"], "tile_nnz": ti["nnz"], "chunks": ti["chunks"],
-                                    "reuse": ti["reuse"], "exact_same": same, "finite": fin}
+                                    "reuse": ti["reuse"], "wide": ti["wide"], "exact_same": same, "finite": fin}
                 base = out[str(ref)]["ms"]
                 for md in modes:
                     out[str(md)]["speedup"] = round(base / out[str(md)]["ms"], 3)
