@@ -149,7 +149,7 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
  * in LDS once; every tile row is still one left-to-right FMA chain in CSR order (exact).  out has 7 slots:
  * out[0]=tiles, out[1]=rows in tiles, out[2]=nonzeros in tiles, out[3]=chunks (LDS fills), out[4]=the sampled
  * mean reuse (nonzeros per union column) x 1000 the policy decided on, out[5]=1 when tiles run in XCD order,
- * out[6]=1 when tiles use 32-byte compute lanes (SPMM_HIP_TILE_WIDE).
+ * out[6]=the tile kernel's compute-lane width in 16-byte pieces of a B row (1, 2, 4; SPMM_HIP_TILE_WIDE=<S>).
  * SPMM_HIP_TILES=-1 disables tiles, =1 takes every eligible tile; SPMM_HIP_TILE_REUSE=<x> sets the threshold. */
 int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out);
 

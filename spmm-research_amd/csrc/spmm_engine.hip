@@ -63,7 +63,7 @@ constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may
 #endif
 constexpr int TILE_UCB = SPMM_TILE_UCB_KB * 1024;   // LDS bytes of staged B rows per chunk (two chunk buffers per workgroup)
 constexpr int TILE_CAPA = SPMM_TILE_CAPA;           // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
-constexpr int TILE_WIDE_DEFAULT = 0;      // SPMM_HIP_TILE_WIDE: 32-byte compute lanes in tile mode
+constexpr int TILE_WIDE_DEFAULT = 1;      // SPMM_HIP_TILE_WIDE: tile compute-lane width, 16-byte pieces
 constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
 constexpr double TILE_MIN_REUSE = 8.0;    // policy: sampled reuse (nnz per union column) to leave the row kernel (§6.9)
 constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgroup each) to fill 256 CUs twice (§6.9:
@@ -102,7 +102,7 @@ struct Plan {
     int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
     int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
     int tile_xcd = 0;          // tiles in XCD-contiguous order
-    int tile_wide = 0;         // 32-byte compute lanes (two 16-byte pieces of a B row per lane), where RPG allows
+    int tile_wide = 1;         // compute-lane width in 16-byte pieces of a B row (1, 2, 4), where RPG allows
     int64_t tile_rows = 0, tile_nnz = 0, tile_chunks = 0;
     double tile_reuse = 0.0;   // sampled mean reuse (nnz per union column) the policy saw
 };
@@ -347,11 +347,13 @@ void launch_tiles_g(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t
     };
     using S1 = std::integral_constant<int, 1>;
     using S2 = std::integral_constant<int, (RPG % 2 == 0 && G >= 2) ? 2 : 1>;
-    if (h->plan.tile_wide) {
-        if (h->plan.tile_xcd) go(std::true_type(), S2()); else go(std::false_type(), S2());
-    } else {
-        if (h->plan.tile_xcd) go(std::true_type(), S1()); else go(std::false_type(), S1());
-    }
+    using S4 = std::integral_constant<int, (RPG % 4 == 0 && G >= 4) ? 4 : 1>;
+    auto go_x = [&](auto s_c) {
+        if (h->plan.tile_xcd) go(std::true_type(), s_c); else go(std::false_type(), s_c);
+    };
+    if (h->plan.tile_wide == 4) go_x(S4());
+    else if (h->plan.tile_wide == 2) go_x(S2());
+    else go_x(S1());
 }
 
 template <typename T>
@@ -1183,7 +1185,11 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             // consecutive tiles share most of their columns: in XCD order they share an L2 as well
             const int env_x = env_int("SPMM_HIP_TILE_XCD", 1);
             pl.tile_xcd = (env_x > 0 && pl.ntile >= 64) ? 1 : 0;
-            pl.tile_wide = (env_int("SPMM_HIP_TILE_WIDE", TILE_WIDE_DEFAULT) > 0 && tile_rpg(g_t) % 2 == 0) ? 1 : 0;
+            // compute-lane width in 16-byte pieces: the requested 1/2/4, lowered until rows per group divide
+            int sw = std::max(1, env_int("SPMM_HIP_TILE_WIDE", TILE_WIDE_DEFAULT));
+            sw = sw >= 4 ? 4 : sw >= 2 ? 2 : 1;
+            while (sw > 1 && tile_rpg(g_t) % sw != 0) sw /= 2;
+            pl.tile_wide = sw;
         }
     }
 

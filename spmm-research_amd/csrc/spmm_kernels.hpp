@@ -526,9 +526,9 @@ __device__ __forceinline__ void dma_to_lds(const char *src, char *dst, int bytes
 // staging, not LDS-DMA: a DMA in flight makes the compiler wait for lgkmcnt(0) at every LDS read of the compute
 // (measured: 0.243 vs 0.253 ms on the 39120 x 500 dense band).
 //
-// S = 16-byte pieces of a B row per compute lane (1, or 2 = "wide" lanes): G/S lanes per row group and RPG rows per
-// group (the host passes RPG / S, so the tile geometry NG x RPG -- and with it the inspector's layout -- is the same);
-// wide lanes halve the broadcast reads of values and offsets per FMA.  Staging always moves 16-byte pieces.
+// S = 16-byte pieces of a B row per compute lane (1, or 2 / 4 = "wide" lanes): G/S lanes per row group and RPG rows
+// per group (the host passes RPG / S, so the tile geometry NG x RPG -- and with it the inspector's layout -- is the
+// same); wide lanes divide the broadcast reads of values and offsets per FMA by S.  Staging moves 16-byte pieces.
 template <typename T, int VEC, int G, int RPG, int UCB, int CAPA, bool NTC, bool XCD, int S = 1>
 __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__restrict__ tiles,
                                                           const int4 *__restrict__ tchunk,
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
     constexpr int GC = G / S;                      // compute lanes per row group
     constexpr int NG = WG / GC;
     constexpr int RMAX = NG * RPG;
-    static_assert(S == 1 || S == 2, "16- or 32-byte compute lanes");
+    static_assert(S == 1 || S == 2 || S == 4, "16-, 32- or 64-byte compute lanes");
     static_assert(GC >= 1 && G % S == 0, "lanes");
     constexpr int NPL = UCB / 16 / WG;             // B pieces per lane per chunk
     constexpr int NPV = (CAPA * (int)sizeof(T) / 16 + WG - 1) / WG;   // value pieces per lane

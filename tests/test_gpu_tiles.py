@@ -181,18 +181,21 @@ def test_tile_policy_gates(env, monkeypatch):
 @pytest.mark.parametrize("line", MATS[:2], ids=["similar", "dense"])
 @pytest.mark.parametrize("k", [16, 32, 64, 128])
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_tiles_wide_lanes_bitexact(env, monkeypatch, line, k, dtype):
-    """32-byte compute lanes (SPMM_HIP_TILE_WIDE=1: two 16-byte pieces of a B row per lane, half the lanes per row,
-    same tile geometry) compute the same FMA chains: bit-identical to 16-byte lanes and to the oracle."""
+@pytest.mark.parametrize("sw", [2, 4])
+def test_tiles_wide_lanes_bitexact(env, monkeypatch, line, k, dtype, sw):
+    """Wide compute lanes (SPMM_HIP_TILE_WIDE=S: S 16-byte pieces of a B row per lane, 1/S the lanes per row, same
+    tile geometry) compute the same FMA chains: bit-identical to 16-byte lanes and to the oracle.  The width drops
+    to what the rows per group allow (B rows >= 128 B for S=2, >= 256 B for S=4)."""
     torch, S, O = env
     A = S.generate(S.gen_params(line))
     x = O.drand48(11 + k, A.ncols * k)
     vals = A.values if dtype == "f64" else A.values.astype(np.float32)
     xx = x if dtype == "f64" else x.astype(np.float32)
-    y1, t1, ex1, _ = run(S, A, vals, xx, k, 1, monkeypatch, {"SPMM_HIP_TILE_WIDE": "1"})
-    y0, t0, ex0, _ = run(S, A, vals, xx, k, 1, monkeypatch, {"SPMM_HIP_TILE_WIDE": "0"})
-    assert t1["tiles"] > 0 and t0["tiles"] == t1["tiles"] and t0["wide"] == 0
-    assert t1["wide"] == int(k * vals.itemsize >= 128)   # wide lanes need >= 2 rows per group (B rows >= 128 B)
+    y1, t1, ex1, _ = run(S, A, vals, xx, k, 1, monkeypatch, {"SPMM_HIP_TILE_WIDE": str(sw)})
+    y0, t0, ex0, _ = run(S, A, vals, xx, k, 1, monkeypatch, {"SPMM_HIP_TILE_WIDE": "1"})
+    assert t1["tiles"] > 0 and t0["tiles"] == t1["tiles"] and t0["wide"] == 1
+    rb = k * vals.itemsize
+    assert t1["wide"] == (sw if rb >= 64 * sw else 2 if rb >= 128 else 1)
     assert np.array_equal(ex0, ex1)
     assert np.array_equal(bits(y1), bits(y0))
     check(O, A, vals, xx, k, y1, ex1)

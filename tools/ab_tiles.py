@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--k", default="32")
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--modes", default="-1,0,1",
-                    help="SPMM_HIP_TILES values; a 'w' suffix (e.g. 1w) adds SPMM_HIP_TILE_WIDE=1, others get =0")
+                    help="SPMM_HIP_TILES values; a 'w<S>' suffix (e.g. 1w2) sets SPMM_HIP_TILE_WIDE=<S>, others get 1")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--env", default="", help="extra KEY=VAL;KEY=VAL for the tile handles")
@@ -54,10 +54,11 @@ def main():
                 vals = A.values.astype(npdt)
                 hs = {}
                 for md in modes:
-                    os.environ["SPMM_HIP_TILES"] = md.rstrip("w")
-                    os.environ["SPMM_HIP_TILE_WIDE"] = "1" if md.endswith("w") else "0"
+                    tm, _, sw = md.partition("w")
+                    os.environ["SPMM_HIP_TILES"] = tm
+                    os.environ["SPMM_HIP_TILE_WIDE"] = sw or "1"
                     for kk, vv in extra.items():
-                        if int(md.rstrip("w")) >= 0:
+                        if int(tm) >= 0:
                             os.environ[kk] = vv
                         else:
                             os.environ.pop(kk, None)
