@@ -65,6 +65,8 @@ constexpr int TILE_UCB = SPMM_TILE_UCB_KB * 1024;   // LDS bytes of staged B row
 constexpr int TILE_CAPA = SPMM_TILE_CAPA;           // entries per chunk (LDS; a multiple of 8; 3 workgroups per CU incl. 512-B granules)
 constexpr int TILE_WIDE_DEFAULT = 1;      // SPMM_HIP_TILE_WIDE: tile compute-lane width, 16-byte pieces
 constexpr int TILE_RMAX = 64;             // rows per tile (row groups x rows per group)
+constexpr int64_t TILE_POLICY_MAX_ROW = 256;   // policy: staged B rows of at most 256 B (K=64 fp64 lost 6-26 %, §6.9)
+constexpr int TILE_MIN_BUILT = 64;         // policy: fewer built tiles than this run as one serial tail (§6.9)
 constexpr double TILE_MIN_REUSE = 8.0;    // policy: sampled reuse (nnz per union column) to leave the row kernel (§6.9)
 constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgroup each) to fill 256 CUs twice (§6.9:
                                           // 76-173 tiles ran 2.7-3x slower than the row kernel's split rows)
@@ -1170,11 +1172,12 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                 const char *thr = getenv("SPMM_HIP_TILE_REUSE");
                 const double min_reuse = forced > 0 ? 1.0 : (thr && *thr) ? atof(thr) : TILE_MIN_REUSE;
                 pl.tile_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax);
-                const bool enough = (h->m + rmax - 1) / rmax >= TILE_MIN_TILES;
+                const bool enough = (h->m + rmax - 1) / rmax >= TILE_MIN_TILES && srow <= TILE_POLICY_MAX_ROW;
                 if (forced > 0 || (enough && pl.tile_reuse >= min_reuse))
                     tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax,
                                         (int)(TILE_UCB / srow), TILE_CAPA, min_reuse, tp,
                                         tile_colmax_for(h->vsize, g_t) - 4, TILE_DMAX - 1);
+                if (tiles && forced <= 0 && (int64_t)tp.tiles.size() < TILE_MIN_BUILT) tiles = false;
             }
         }
         if (tiles) {

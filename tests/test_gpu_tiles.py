@@ -199,3 +199,20 @@ def test_tiles_wide_lanes_bitexact(env, monkeypatch, line, k, dtype, sw):
     assert np.array_equal(ex0, ex1)
     assert np.array_equal(bits(y1), bits(y0))
     check(O, A, vals, xx, k, y1, ex1)
+
+
+def test_tile_policy_row_bytes(env, monkeypatch):
+    """The default policy stages B rows of at most 256 bytes: the same high-reuse band that takes
+    tiles at K=32 fp64 (256-B rows) keeps the row kernel at K=64 (512-B rows measured 6-26 % slower in tiles) and
+    at K=64 fp32 (256-B rows) takes them again; forcing still tiles any eligible shape."""
+    torch, S, O = env
+    monkeypatch.delenv("SPMM_HIP_TILES", raising=False)
+    A = S.generate(S.gen_params("22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14"))
+    for k, vals, want in ((32, A.values, True), (64, A.values, False), (64, A.values.astype(np.float32), True)):
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, k, 0)
+        assert (mf.tile_info()["tiles"] > 0) == want, (k, vals.dtype)
+        mf.close()
+    monkeypatch.setenv("SPMM_HIP_TILES", "1")
+    mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, 64, 0)
+    assert mf.tile_info()["tiles"] > 0
+    mf.close()
