@@ -29,12 +29,12 @@ struct HipPipe : Matrix_Format
 {
 	spmm_sddmm_t * sd;
 	spmm_hip_t * h[4];                      // 'K', 'Q', 'V', final
-	const INT_T * key[4];                   // the row_ptr each handle was built from
+	struct Key { const INT_T * ia; const INT_T * ja; INT_T m, k, nnz; } key[4];   // what each handle was built from
 	ValueType * K; ValueType * Q; INT_T krows;
 	int dev;
 	HipPipe(long m, long n, long nnz) : Matrix_Format(m, n, nnz), sd(NULL), K(NULL), Q(NULL), krows(0), dev(0)
 	{
-		for (int i = 0; i < 4; i++) { h[i] = NULL; key[i] = NULL; }
+		for (int i = 0; i < 4; i++) { h[i] = NULL; key[i] = Key{NULL, NULL, 0, 0, 0}; }
 	}
 	~HipPipe() { for (int i = 0; i < 4; i++) spmm_hip_destroy(h[i]); spmm_sddmm_destroy(sd); }
 
@@ -44,13 +44,19 @@ struct HipPipe : Matrix_Format
 		const int s = type == 'K' ? 0 : type == 'Q' ? 1 : type == 'V' ? 2 : 3;
 		const int dt = sizeof(ValueType) == 8 ? SPMM_HIP_F64 : SPMM_HIP_F32;
 		int st;
-		if (!h[s] || key[s] != ia) {
+		// a handle is reused only for the same pattern (arrays AND sizes: a new matrix allocated at a freed address
+		// must not inherit a stale plan); its values are re-uploaded on every call, since the caller may pass new
+		// values in the same arrays (the final SpMM always does: the SDDMM output, sddmm_bench.cpp:934-936)
+		const Key want = {ia, ja, m, k, ia[m]};
+		const Key & have = key[s];
+		if (!h[s] || have.ia != want.ia || have.ja != want.ja || have.m != want.m || have.k != want.k ||
+		    have.nnz != want.nnz) {
 			spmm_hip_destroy(h[s]);
 			h[s] = NULL;
 			if ((st = spmm_hip_create(ia, ja, a, m, k, ia[m], n, dt, dev, &h[s])))
 				die("spmm_hip_create", st, spmm_hip_last_error_detail());
-			key[s] = ia;
-		} else if (s == 3 && (st = spmm_hip_update_values(h[s], a))) {    // final: the SDDMM output as values
+			key[s] = want;
+		} else if ((st = spmm_hip_update_values(h[s], a))) {
 			die("spmm_hip_update_values", st, spmm_hip_last_error_detail());
 		}
 		if ((st = spmm_hip_run_rowmajor(h[s], x, y, n)))

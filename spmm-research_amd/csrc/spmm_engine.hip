@@ -441,6 +441,7 @@ struct Inspection {
     std::vector<int64_t> perm;      // chained mode: position in the window-major arrays -> original nonzero
     int heavy = 0;  // blocks moved to the front of the table
     int nslots = 0;
+    int64_t ngaps = 0;  // gap virtual rows (runs of rows computed by the tile kernel, never in a block)
 };
 
 // Pack virtual rows [v0, v1) greedily into blocks of <= cap nonzeros and <= CAP_ROWS virtual rows, appended to out.
@@ -513,6 +514,7 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool
         }
     }
     if (!any_split && gaps.empty()) out.vdest.clear();
+    out.ngaps = (int64_t)gaps.size();
     const int64_t nv = (int64_t)out.vrow_ptr.size() - 1;
     int64_t v0 = 0;
     for (int64_t gv : gaps) {
@@ -941,6 +943,21 @@ bool build_tiles(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols
     return !tp.tiles.empty();
 }
 
+// The tile tables are addressed with 32-bit positions (chunk descriptors' first entry / column / segment, the
+// kernel's tval + ch.z, d_tperm): every padded table must stay below 2^31 entries.  Each row segment is padded to
+// 4 entries in every chunk it touches, so the padded count can be well above nnz (a ~1.3e9-nonzero short-row
+// matrix would overflow).  SPMM_HIP_TILE_INDEX_LIMIT lowers the limit (tests of this guard only).
+int64_t tile_index_limit() {
+    const char *v = getenv("SPMM_HIP_TILE_INDEX_LIMIT");
+    const long long l = (v && *v) ? atoll(v) : 0;
+    return l > 0 ? std::min<int64_t>(l, INT32_MAX) : (int64_t)INT32_MAX;
+}
+bool tile_tables_fit(const TilePlan &tp) {
+    const int64_t lim = tile_index_limit(), pad = PAD_BYTES;
+    return (int64_t)tp.perm.size() + pad < lim && (int64_t)tp.tseg.size() + pad < lim &&
+           (int64_t)tp.tcol.size() + pad < lim && (int64_t)tp.chunks.size() < lim;
+}
+
 // Policy gate: mean reuse over <= 256 evenly spaced candidate tiles (cheap; the full build only runs when tiles can
 // pay).  Returns the sampled mean reuse.
 double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int rmax) {
@@ -1178,6 +1195,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                                         (int)(TILE_UCB / srow), TILE_CAPA, min_reuse, tp,
                                         tile_colmax_for(h->vsize, g_t) - 4, TILE_DMAX - 1);
                 if (tiles && forced <= 0 && (int64_t)tp.tiles.size() < TILE_MIN_BUILT) tiles = false;
+                if (tiles && !tile_tables_fit(tp)) tiles = false;     // 32-bit tile positions (row kernel instead)
             }
         }
         if (tiles) {
@@ -1240,16 +1258,18 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         lane_layout(pl.kw, k, h->vsize, vec, g);
         const int ng = WG / g;
         const int lcap = std::max(1, 64 / g);
-        const double nvr = (double)(in.vrow_ptr.size() - 1);
+        // the rows the row kernel runs: gap virtual rows and the tile rows' nonzeros are not among them
+        const double nvr = (double)((int64_t)in.vrow_ptr.size() - 1 - in.ngaps);
+        const double nnz_rows = (double)(h->nnz - (tiles ? tp.nnz : 0));
         const double rows_per_block = in.blk.empty() ? 0.0 : nvr / (double)in.blk.size();
-        const double mean_vrow = nvr > 0 ? (double)h->nnz / nvr : 0.0;
+        const double mean_vrow = nvr > 0 ? nnz_rows / nvr : 0.0;
         const int env_l = env_int("SPMM_HIP_LANES", 0);
         const int forced = h->var.lanes != 0 ? h->var.lanes : env_l;
         bool all_blocks = false;
         if (forced != 0)
             all_blocks = forced > 0, pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
         else
-            all_blocks = h->nnz > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW,
+            all_blocks = nnz_rows > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW,
             pl.lmax = all_blocks ? lcap : 1;
         // flag the blocks that may use vector lanes: all of them under the policy, else (unless disabled) the blocks
         // made only of split-row pieces (inexact anyway; a 16 M-nonzero row is thousands of one-piece blocks)
@@ -1495,16 +1515,32 @@ int spmm_hip_run_device_batch(int32_t count, spmm_hip_t *const *hs, const void *
     }
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(hipEventRecord(pool.fork, s));
-    for (int i = 1; i < count; ++i) {
-        HIPCHK(hipStreamWaitEvent(pool.side[i - 1], pool.fork, 0));
-        int st = spmm_hip_run_device(hs[i], d_b[i], b_layout[i], d_c[i], k[i], pool.side[i - 1]);
-        if (st != SPMM_HIP_OK) return st;
-        HIPCHK(hipEventRecord(pool.join[i - 1], pool.side[i - 1]));
+    // From here on every side stream that joined the fork is joined back into `stream` even when a run fails, so
+    // a graph capture on `stream` stays well formed and the first error is what the caller sees.
+    int first = SPMM_HIP_OK;
+    std::string first_detail;
+    auto keep = [&](int st) {
+        if (st != SPMM_HIP_OK && first == SPMM_HIP_OK) first = st, first_detail = g_detail;
+    };
+    std::vector<char> forked((size_t)count, 0);
+    for (int i = 1; i < count && first == SPMM_HIP_OK; ++i) {
+        hipError_t e = hipStreamWaitEvent(pool.side[i - 1], pool.fork, 0);
+        if (e != hipSuccess) {
+            keep(fail(SPMM_HIP_ERR_HIP, std::string("hipStreamWaitEvent(fork): ") + hipGetErrorString(e)));
+            break;
+        }
+        forked[(size_t)i] = 1;
+        keep(spmm_hip_run_device(hs[i], d_b[i], b_layout[i], d_c[i], k[i], pool.side[i - 1]));
     }
-    int st = spmm_hip_run_device(hs[0], d_b[0], b_layout[0], d_c[0], k[0], s);
-    if (st != SPMM_HIP_OK) return st;
-    for (int i = 1; i < count; ++i) HIPCHK(hipStreamWaitEvent(s, pool.join[i - 1], 0));
-    return SPMM_HIP_OK;
+    if (first == SPMM_HIP_OK) keep(spmm_hip_run_device(hs[0], d_b[0], b_layout[0], d_c[0], k[0], s));
+    for (int i = 1; i < count; ++i) {
+        if (!forked[(size_t)i]) continue;
+        hipError_t e = hipEventRecord(pool.join[i - 1], pool.side[i - 1]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, pool.join[i - 1], 0);
+        if (e != hipSuccess) keep(fail(SPMM_HIP_ERR_HIP, std::string("batch join: ") + hipGetErrorString(e)));
+    }
+    if (first != SPMM_HIP_OK) g_detail = first_detail;
+    return first;
 }
 
 }  // extern "C"
@@ -1790,6 +1826,8 @@ int spmm_hip_debug_tiles(const int32_t *row_ptr, const int32_t *col_idx, int64_t
     TilePlan tp;
     build_tiles(row_ptr, col_idx, m, ncols, T, rmax, uc, capa, min_reuse, tp, colmax > 0 ? colmax : INT32_MAX,
                 dmax > 0 ? dmax : INT32_MAX);
+    if (!tile_tables_fit(tp))        // the plan would turn tiles off here (32-bit tile positions)
+        return fail(SPMM_HIP_ERR_OVERFLOW, "debug_tiles: tile tables exceed the 32-bit position range");
     auto dup = [](const auto &v) {
         using E = typename std::decay_t<decltype(v)>::value_type;
         E *p = (E *)malloc(std::max<size_t>(v.size(), 1) * sizeof(E));

@@ -10,6 +10,8 @@ What it writes (data only -- inputs and the reference's outputs; no reference so
   smtx_csr.npz              per DLMC .smtx (tests/golden/smtx/): the offsets / columns smtx_read returns
   mtx_csr.npz               per .mtx: the CSR that mtx_read + coo_to_csr produce (spmv_bench.cpp:724-826), and
                             C = A*B from the reference plugin for K in {1,4,32} with B = 1 and B = drand48(42)
+  mtx_csr_f32.npz           the same from the reference's FLOAT build (ValueType=float): values as it reads them,
+                            C for K in {1,4,32} with x = (float) drand48(42)
   spmm_cases.npz            seeded random CSRs (empty rows, a long row, a zero-nnz matrix) and the reference
                             plugin's C for fp64 and fp32 at K in {1,8,32,128}
   partition.npz             loop_partitioner_balance_prefix_sums boundaries for several row_ptr / worker counts
@@ -157,6 +159,27 @@ def make_mtx_fixtures():
                 y = O.ref_spmm(rp, ci, va.copy(), n, x, k)
                 out[f"{key}.y.k{k}.{bname}"] = y
     np.savez_compressed(OUT / "mtx_csr.npz", **out)
+
+
+def make_mtx_f32_fixtures():
+    """The fp32 drop-in pin (ValueType=float, make.sh:98-102): per .mtx, the CSR values the reference's FLOAT build
+    reads (mtx_read with MATRIX_MARKET_FLOAT_T=float) and C = A*B from its float plugin at K in {1, 4, 32} with
+    x = (float) drand48(42) -- the x the fp32 harness / refabi_driver_f hands the plugin."""
+    O.ref_lib("f").ref_set_threads(1)
+    out = {}
+    for name in sorted(MTX_FILES):
+        m, n, rp, ci, va = O.ref_mtx_to_csr(str(MTX / name), "f")
+        vf = va.astype(np.float32)
+        assert np.array_equal(vf.astype(np.float64), va), name          # the float build's values, exactly
+        key = name[:-4]
+        out[f"{key}.shape"] = np.array([m, n], np.int64)
+        out[f"{key}.row_ptr"] = rp
+        out[f"{key}.col_idx"] = ci
+        out[f"{key}.vals"] = vf
+        for k in (1, 4, 32):
+            x = O.drand48(42, n * k).astype(np.float32)
+            out[f"{key}.y.k{k}.drand48"] = O.ref_spmm(rp, ci, vf.copy(), n, x, k)
+    np.savez_compressed(OUT / "mtx_csr_f32.npz", **out)
 
 
 SMTX = ROOT / "tests" / "golden" / "smtx"
@@ -322,8 +345,14 @@ def make_features():
 def main():
     if not O.ref_available("d"):
         raise SystemExit("oracle/_ref not built: run `make -C oracle` in a container with /root/reference")
+    only = sys.argv[1:]
+    if only:                       # e.g. `make_golden.py make_mtx_f32_fixtures`: regenerate named fixtures only
+        for fn in only:
+            globals()[fn]()
+        return
     write_mtx()
     make_mtx_fixtures()
+    make_mtx_f32_fixtures()
     make_smtx_fixtures()
     make_spmm_cases()
     make_partition()

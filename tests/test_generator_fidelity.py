@@ -76,7 +76,7 @@ def _nn_reachable(req):
 
 
 def _lines(size_index, every):
-    from medium_dataset import medium_dataset_lines
+    from spmm_amd.datasets import medium_dataset_lines
     lines = medium_dataset_lines()
     size = lambda l: (int(l.split()[0]) * (12 * int(l.split()[2]) + 4)) // (1 << 20)   # noqa: E731
     sizes = sorted({size(l) for l in lines})

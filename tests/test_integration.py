@@ -69,15 +69,19 @@ def test_plugin_drives_engine_bitexact(golden, tmp_path, k):
 
 
 @pytest.mark.gpu
-def test_plugin_f32_drives_engine(golden, tmp_path):
+@pytest.mark.parametrize("k", [1, 4, 32])
+def test_plugin_f32_drives_engine_bitexact(golden, tmp_path, k):
+    """The fp32 drop-in (refabi_driver_f = the plugin compiled with ValueType=float) against the reference's own
+    FLOAT build (mtx_csr_f32.npz, tests/golden/make_golden.py): bit for bit."""
     assert _exe("f").exists()
-    g = golden("mtx_csr.npz")
+    g = golden("mtx_csr_f32.npz")
     for path in MTX:
         name = path.stem
-        out = tmp_path / f"{name}.bin"
-        r = subprocess.run([str(_exe("f")), str(path), "32", str(out)], capture_output=True, text=True, timeout=120)
+        out = tmp_path / f"{name}.{k}.bin"
+        r = subprocess.run([str(_exe("f")), str(path), str(k), str(out)], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         m = int(g[f"{name}.shape"][0])
-        y = np.fromfile(out, np.float32).reshape(m, 32).astype(np.float64)
-        want = g[f"{name}.y.k32.drand48"]
-        assert np.allclose(y, want, rtol=1e-5, atol=1e-5), name
+        y = np.fromfile(out, np.float32).reshape(m, k)
+        want = g[f"{name}.y.k{k}.drand48"]
+        assert want.dtype == np.float32
+        assert np.array_equal(y.view(np.int32), want.view(np.int32)), name

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from conftest import GOLDEN
 
 
 def _cases(d):
@@ -38,6 +39,27 @@ def test_spmm_mtx_fixtures_bitwise(golden):
                 x = np.ones(n * k) if b == "ones" else O.drand48(42, n * k)
                 y = O.spmm(rp, ci, va, n, x, k)
                 assert np.array_equal(y.view(np.int64), d[f"{c}.y.k{k}.{b}"].view(np.int64)), (c, k, b)
+
+
+def test_spmm_mtx_fixtures_f32_bitwise(golden):
+    """fp32 pin: the C restatement on the float build's CSR == the reference FLOAT plugin's output; and the engine's
+    host reader (double values, cast to float as the fp32 drivers do) hands the same floats over."""
+    import spmm_amd as S
+    d = golden("mtx_csr_f32.npz")
+    n_checked = 0
+    for c in _cases(d):
+        rp, ci, va = d[f"{c}.row_ptr"], d[f"{c}.col_idx"], d[f"{c}.vals"]
+        assert va.dtype == np.float32
+        m, n = (int(v) for v in d[f"{c}.shape"])
+        A, _, _ = S.mtx_read(GOLDEN / "mtx" / f"{c}.mtx")
+        assert np.array_equal(A.row_ptr, rp) and np.array_equal(A.col_idx, ci), c
+        assert np.array_equal(A.values.astype(np.float32).view(np.int32), va.view(np.int32)), c
+        for k in (1, 4, 32):
+            x = O.drand48(42, n * k).astype(np.float32)
+            y = O.spmm(rp, ci, va, n, x, k)
+            assert np.array_equal(y.view(np.int32), d[f"{c}.y.k{k}.drand48"].view(np.int32)), (c, k)
+            n_checked += 1
+    assert n_checked >= 30
 
 
 def test_partition_matches_reference(golden):

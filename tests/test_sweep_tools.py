@@ -6,7 +6,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
 
 
 def test_medium_dataset_lines_match_published_set():
-    from medium_dataset import medium_dataset_lines, sorted_sha256, SHA256_SORTED
+    from spmm_amd.datasets import medium_dataset_lines, sorted_sha256, SHA256_SORTED
     L = medium_dataset_lines()
     assert len(L) == 16190 and len(set(L)) == 16190
     assert sorted_sha256(L) == SHA256_SORTED

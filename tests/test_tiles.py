@@ -107,3 +107,23 @@ def test_tile_unsorted_rejected(S):
     rp = np.array([0, 3], np.int32)
     with pytest.raises(S.SpmmHipError):
         S.debug_tiles(rp, np.array([2, 1, 0], np.int32), 3, 2048)
+
+
+def test_tile_index_guard(S, monkeypatch):
+    """tile tables use 32-bit positions; a decomposition whose padded tables reach the limit is refused
+    (the plan then keeps those rows in the row kernel).  The limit is lowered here so a small matrix reaches it."""
+    rng = np.random.default_rng(3)
+    m, n = 256, 96
+    rows = [np.sort(rng.choice(n, 40, replace=False)) for _ in range(m)]
+    rp = np.zeros(m + 1, np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    t = S.debug_tiles(rp, col, n, 2048, 32, 48, 896, 1.0)
+    nz = len(t["perm"])
+    assert nz >= rp[-1]
+    monkeypatch.setenv("SPMM_HIP_TILE_INDEX_LIMIT", str(nz))          # padded positions + 64 >= limit: refused
+    with pytest.raises(S.SpmmHipError) as e:
+        S.debug_tiles(rp, col, n, 2048, 32, 48, 896, 1.0)
+    assert e.value.status == -7
+    monkeypatch.setenv("SPMM_HIP_TILE_INDEX_LIMIT", str(nz + 4096))   # within the limit: accepted
+    assert len(S.debug_tiles(rp, col, n, 2048, 32, 48, 896, 1.0)["perm"]) == nz

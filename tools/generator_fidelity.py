@@ -53,7 +53,7 @@ def measure(line: str) -> dict:
 
 
 def main():
-    from medium_dataset import medium_dataset_lines
+    from spmm_amd.datasets import medium_dataset_lines
     ap = argparse.ArgumentParser()
     ap.add_argument("--size-index", type=int, default=0, help="which matrix size of the dataset (0 = smallest)")
     ap.add_argument("--every", type=int, default=1, help="take every n-th line of that size")

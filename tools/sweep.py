@@ -38,7 +38,7 @@ def dataset_lines(args) -> list[str]:
     if args.dataset == "twins":
         lines = list(json.loads((ROOT / "spmm-research_amd" / "spmm_amd" / "validation_twins.json").read_text())["twins"].values())
     elif args.dataset == "medium":
-        from medium_dataset import medium_dataset_lines
+        from spmm_amd.datasets import medium_dataset_lines
         lines = medium_dataset_lines()
     else:
         lines = [l.strip() for l in open(args.dataset) if l.strip()]
