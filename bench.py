@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""bench.py -- headline benchmark: CSR SpMM C = A*B, K=32, fp64, synthetic matrix, MI355X.
+"""bench.py -- headline benchmark: CSR SpMM C = A*B, K=32, fp64, synthetic matrices, MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  N>1 runs one rank per GPU; when it is not
 started by torch.distributed.run (no WORLD_SIZE in the environment) it starts torch.distributed.run itself as a
@@ -7,46 +7,52 @@ CHILD process (before anything touches the GPU) and exits with its status.  A wo
 is an error (exit 2).  One "step" = one SpMM over the rank's row shard, inputs resident in HBM.  Rank 0 prints ONE
 JSON line.
 
-Workloads (--workload):
-  config2   (default; BASELINE.json configs[1]) generator line
-            1000000 1000000 20 6.6667 normal random 0.3 100 0.95 0.5 14
-            (1M x 1M, avg 20 nnz/row, normal row lengths, bw 0.3, skew 100, neighbours 0.95, cross-row similarity
-            0.5, seed 14).
-  config4    the largest avg-20 skew-10^4 line of synthetic_matrices_large_dataset.txt with
-            gamma row lengths: 7477550 7477550 20 6.6667 gamma random 0.3 10000 0.95 0.5 14 (150 M nonzeros).
-  medium-sample  (config 3) every --sample-stride-th line of synthetic_matrices_medium_dataset (N=1 only); value =
-            aggregate GFLOP/s over the sample (sum of flops / sum of kernel time).
-  pipeline   the sparse-attention pipeline consumer, fp32, n=512: K/Q/V = W x (DLMC-like 512 x 512
-            attention weights, 70 % pruned), SDDMM over a band+random mask (band 16, 5 % dense), final SpMM;
-            one step = the reference compute() step (pipeline_code_bench/sddmm_bench.cpp:918-937), HBM-resident,
-            captured in a hipGraph; GFLOP/s by the reference formula (:978-983).  N=1 only.
-A values: the generator's seeded U[0.5, 1.5).  B: drand48(seed 42), drawn on the host in the reference harness's
-column-major layout [K][ncols] (the same x the CPU baseline multiplies), uploaded transposed to the engine's
-row-major layout, resident in HBM.
+The line (default, --workload config2):
+  value     config 2 (BASELINE.json configs[1]): generator line
+            1000000 1000000 20 6.6667 normal random 0.3 100 0.95 0.5 14, K=32 fp64 -- the same fixed matrix at every
+            N, split N ways (strong scaling), so the driver's 1/2/4/8 values form one curve.  value = 2*nnz*K*steps /
+            (max over ranks of the HIP-event time of the K timed steps on the launch stream); the
+            barrier-inclusive wall time is reported beside it ("wall_ms_per_step").
+  dataset   (N=1 only; --no-dataset skips it) the metric's own workload, BASELINE "synthetic medium dataset, K=32
+            fp64": every --dataset-stride-th line of synthetic_matrices_medium_dataset (stride 160 = 102 matrices),
+            per matrix `--dataset-iters` HIP-event-timed launches; aggregate GFLOP/s (sum flops / sum time), median /
+            p10 / p90 roofline fraction, per-matrix PMC traffic when profiles/ holds it for this engine build, an
+            achievable-ceiling fraction, and a cpu_baseline on a time-bounded subset of the same matrices (same A and
+            B).  "scaling": "single-gpu".
+Other workloads (N=1 unless noted):
+  config4   (N >= 1) the largest avg-20 skew-10^4 line of synthetic_matrices_large_dataset.txt with gamma row lengths
+            (7477550 rows, 150 M nonzeros).
+  medium-sample  the dataset record above as the line itself.
+  twins     (config 5) the 52 validation twins (reference config.sh:283-339) at K=32, fp64 AND fp32: per dtype
+            aggregate GFLOP/s and median fraction, and a cpu_baseline on every twin in the same run (time-bounded).
+  pipeline   the sparse-attention pipeline consumer, fp32, n=512 (see run_pipeline).
 
-Multi-GPU (--scaling, default strong): STRONG = one fixed global matrix (the workload's line) split into N
-nnz-balanced row ranges with the reference partitioner loop_partitioner_balance_prefix_sums
-(lib/parallel_util.h:141-165); the same matrix at every N, so the driver's 1/2/4/8 values form a strong-scaling
-curve.  WEAK = N stacked copies of the line's shape (bw/N).  Each rank generates only its rows; B is broadcast from
-rank 0 over RCCL once at setup (timed, reported); C stays sharded in the timed loop and is all-gathered once
-afterwards (timed, reported).  Per-rank kernel time (HIP events on the launch stream), its max over ranks and the
-nnz imbalance (max/mean) are reported.
+A values: the generator's seeded U[0.5, 1.5).  B: config 2 / config 4: drand48(seed 42) drawn on the host in the
+reference harness's column-major layout [K][ncols] (the x the CPU baseline multiplies), uploaded transposed to the
+engine's row-major layout; dataset / twins: torch.rand(seed 42) on the device (copied back column-major for the
+CPU baseline).  Everything resident in HBM in the timed region.
 
-Self-check (every rank, every run): 256 sampled rows of the rank's C against a host recomputation with numpy
-(normwise 1e-10 fp64 / (n+1)*2^-24 fp32); a failure or a non-finite C exits non-zero.  Bit-exact parity against
-the oracle lives in tests/ (the oracle is test infrastructure and only the cpu_baseline leg below uses it).
+Multi-GPU (--scaling, default strong): STRONG = one fixed global matrix split into N nnz-balanced row ranges with
+the reference partitioner loop_partitioner_balance_prefix_sums (lib/parallel_util.h:141-165).  WEAK = N stacked
+copies of the line's shape (bw/N).  Each rank generates only its rows; B is broadcast from rank 0 once at setup
+(timed); C stays sharded in the timed loop and is all-gathered once afterwards (timed).  --dist-backend gloo (test
+mode) lets several ranks share one GPU (collectives staged through host memory).
 
-JSON extras: "roofline" for the SpMM kernel (algorithmic bytes per launch -- SURVEY §8d, one definition at every N:
-the rank's rows and nonzeros with the global column count -- over the HIP-event-timed launch duration),
-"cpu_baseline" (oracle/liboracle.so, the bit-pinned C restatement of the reference compute_csr, timed on this
-host at N=1 on the same A and B: 100 warm-up calls like the reference harness, then timed calls, median),
-"setup" (generation, B broadcast, C all-gather), "plugin_e2e" (N=1: the reference-contract call with host x / y:
-H2D + transpose + kernel + D2H).
+Self-check (every rank, every run): sampled rows of the rank's C against a numpy recomputation (normwise 1e-10
+fp64 / (n+1)*2^-24 fp32); a failure or a non-finite C exits non-zero.  Bit-exact parity against the oracle lives in
+tests/ (the oracle is test infrastructure; only the cpu_baseline legs use it).
+
+roofline: algorithmic bytes per launch (4(m+1) + (4+s)nnz + s*K*ncols + s*K*m) over the HIP-event
+launch time against 8 TB/s; "traffic" = PMC past-L2 bytes per launch (tools/collect_pmc.py, tools/pmc_dataset.py)
+when profiles/ holds them for this engine build; "achievable" = the gather ceiling: that traffic at
+the chip's measured random-row gather rate for a table of B's size, and the L2 requests at the L2-resident gather
+rate (profiles/r01_gather_probe.jsonl) -- "frac_of_achievable" = ceiling time / measured time.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -62,6 +68,12 @@ _AFFINITY0 = os.sched_getaffinity(0)
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "GFLOP/s + achieved HBM GB/s, synthetic medium dataset, CSR SpMM K=32 fp64"
+# random-row gather rates of this chip by table size (profiles/r01_gather_probe.jsonl: 256-B rows, 16 in flight per
+# 16-lane group, all CUs): bytes -> TB/s.  The L2-resident rate bounds the on-chip request path.
+GATHER_PROBE = [(2 << 20, 27.79), (16 << 20, 9.62), (64 << 20, 7.50), (160 << 20, 7.09), (256 << 20, 7.19),
+                (1 << 30, 6.85), (4 << 30, 5.86)]
+L2_GATHER_TBS = 27.79
+L2_LINE = 128
 
 
 def parse():
@@ -71,7 +83,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
-    ap.add_argument("--workload", choices=["config2", "config4", "medium-sample", "pipeline"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config4", "medium-sample", "twins", "pipeline"],
+                    default="config2")
     ap.add_argument("--pipe-m", type=int, default=512, help="pipeline: weight rows = mask size")
     ap.add_argument("--pipe-k", type=int, default=512, help="pipeline: weight columns (rows of x)")
     ap.add_argument("--pipe-n", type=int, default=512, help="pipeline: columns of x (NUM_COLS)")
@@ -81,13 +94,23 @@ def parse():
     ap.add_argument("--pipe-mode", type=int, default=0, help="pipeline: SDDMM flags (0 reference, 1 QK^T, |2 softmax)")
     ap.add_argument("--gen", default=None, help="override: 11-field generator line of the global matrix")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
-    ap.add_argument("--sample-stride", type=int, default=160, help="medium-sample: every n-th dataset line")
-    ap.add_argument("--sample-offset", type=int, default=0)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: test mode, ranks may share one GPU (collectives staged through host memory)")
+    ap.add_argument("--dump-c", default=None, help="rank 0 writes a row sample of the (gathered) C + exact mask (npz)")
+    ap.add_argument("--no-dataset", action="store_true", help="skip the medium-dataset sub-record (N=1)")
+    ap.add_argument("--dataset-stride", type=int, default=160, help="dataset: every n-th medium-dataset line")
+    ap.add_argument("--dataset-offset", type=int, default=0)
+    ap.add_argument("--dataset-iters", type=int, default=10, help="dataset / twins: timed launches per matrix")
+    ap.add_argument("--dataset-warmup", type=int, default=3)
+    ap.add_argument("--dataset-cpu-seconds", type=float, default=20.0, help="dataset: CPU-baseline budget")
+    ap.add_argument("--twins-cpu-seconds", type=float, default=1.0, help="twins: CPU-baseline budget per twin/dtype")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-warmup", type=int, default=100, help="CPU-baseline warm-up calls (reference harness: 100)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget of timed CPU-baseline calls")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"),
-                    help="per-launch HBM traffic collected by tools/collect_pmc.py (optional)")
+                    help="config-2 per-launch PMC counters (tools/collect_pmc.py)")
+    ap.add_argument("--pmc-dataset", default=str(ROOT / "profiles" / "pmc_dataset_latest.json"),
+                    help="per-matrix PMC records (tools/pmc_dataset.py), keyed by line, K, dtype and engine build")
     return ap.parse_args()
 
 
@@ -139,10 +162,37 @@ def engine_sha256() -> str:
     import hashlib
     h = hashlib.sha256()
     pkg = ROOT / "spmm-research_amd"
-    for f in (pkg / "csrc" / "spmm_engine.hip", pkg / "csrc" / "spmm_kernels.hpp", ROOT / "include" / "spmm_hip.h",
-              pkg / "Makefile"):
+    for f in (pkg / "csrc" / "spmm_engine.hip", pkg / "csrc" / "spmm_kernels.hpp", pkg / "csrc" / "spmm_handle.hpp",
+              pkg / "csrc" / "spmm_multi.hip", ROOT / "include" / "spmm_hip.h", pkg / "Makefile"):
         h.update(f.read_bytes())
     return h.hexdigest()
+
+
+def gather_rate_tbs(table_bytes: float) -> float:
+    """Measured random-row gather rate (TB/s) for a table of `table_bytes` (log-linear between probe points)."""
+    pts = GATHER_PROBE
+    if table_bytes <= pts[0][0]:
+        return pts[0][1]
+    for (b0, r0), (b1, r1) in zip(pts, pts[1:]):
+        if table_bytes <= b1:
+            f = (math.log(table_bytes) - math.log(b0)) / (math.log(b1) - math.log(b0))
+            return r0 + f * (r1 - r0)
+    return pts[-1][1]
+
+
+def achievable(t_ms: float, traffic: float | None, l2_req: float | None, b_bytes: float) -> dict | None:
+    """The gather ceiling of a launch: its measured past-L2 bytes at the chip's random-row gather rate
+    for a table of B's size, and its L2 requests (x 128 B) at the L2-resident gather rate; the larger time is the
+    ceiling.  frac_of_achievable = ceiling / measured (1.0 = at the ceiling)."""
+    if traffic is None or t_ms <= 0:
+        return None
+    r = gather_rate_tbs(b_bytes)
+    t_past = traffic / (r * 1e12) * 1e3
+    t_l2 = (l2_req * L2_LINE) / (L2_GATHER_TBS * 1e12) * 1e3 if l2_req else 0.0
+    t = max(t_past, t_l2)
+    return {"t_ms": round(t, 5), "bound": "past-L2 gather" if t_past >= t_l2 else "L2 requests",
+            "past_l2_gather_tbs": round(r, 2), "t_past_l2_ms": round(t_past, 5), "t_l2_ms": round(t_l2, 5),
+            "frac_of_achievable": round(t / t_ms, 4)}
 
 
 def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
@@ -185,8 +235,27 @@ def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
                        f"({t_warm:.1f} s) + {len(times)} timed, median {t * 1e3:.1f} ms/call")}
 
 
+def cpu_time_once(A, x_col, k: int, dtype, threads: int, budget_s: float) -> float:
+    """One warm-up + timed calls of the oracle's compute_csr within budget_s (at least one); median seconds."""
+    import numpy as np
+    from oracle import oracle as O
+    L = O.lib()
+    vals = np.ascontiguousarray(A.values, dtype)
+    y = np.zeros(max(A.m, 1) * k, dtype)
+    fn = L.oracle_spmm_csr_d if dtype == np.float64 else L.oracle_spmm_csr_f
+    fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, x_col, y, k, threads)
+    ts = []
+    t_end = time.perf_counter() + budget_s
+    while not ts or (time.perf_counter() < t_end and len(ts) < 5):
+        t0 = time.perf_counter()
+        fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, x_col, y, k, threads)
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2]
+
+
 def selfcheck(A, B_host_rowmajor, C_dev, k: int, dtype, nsample: int = 256, seed: int = 5) -> dict:
-    """numpy recomputation of sampled rows (not the oracle; a sanity check of the run, parity is in tests/)."""
+    """numpy recomputation of sampled rows (not the oracle; a sanity check of the run, parity is in tests/).
+    B_host_rowmajor: host B [ncols][k], or a callable rows -> B rows (e.g. gathered from HBM)."""
     import numpy as np
     rng = np.random.default_rng(seed)
     m = A.m
@@ -196,12 +265,17 @@ def selfcheck(A, B_host_rowmajor, C_dev, k: int, dtype, nsample: int = 256, seed
     rows = np.unique(np.concatenate([rng.choice(m, min(nsample, m), replace=False), [int(np.argmax(deg))]]))
     import torch
     got_all = C_dev[torch.from_numpy(rows).to(C_dev.device)].cpu().numpy().astype(np.float64)
+    cols = np.unique(np.concatenate([A.col_idx[A.row_ptr[r]:A.row_ptr[r + 1]] for r in rows]))
+    if callable(B_host_rowmajor):
+        bsub = B_host_rowmajor(cols).astype(np.float64)
+    else:
+        bsub = B_host_rowmajor[cols].astype(np.float64)
     ok = True
     worst = 0.0
     for i, r in enumerate(rows):
         s, e = int(A.row_ptr[r]), int(A.row_ptr[r + 1])
         got = got_all[i]
-        bv = B_host_rowmajor[A.col_idx[s:e]].astype(np.float64)
+        bv = bsub[np.searchsorted(cols, A.col_idx[s:e])]
         av = A.values[s:e].astype(dtype).astype(np.float64)
         want = av @ bv if e > s else np.zeros(k)
         absdot = np.abs(av) @ np.abs(bv) if e > s else np.zeros(k)
@@ -213,63 +287,196 @@ def selfcheck(A, B_host_rowmajor, C_dev, k: int, dtype, nsample: int = 256, seed
     return {"rows": int(len(rows)), "ok": ok, "max_err_over_bound": round(worst, 6)}
 
 
-def run_medium_sample(args, torch, S, np):
-    """config 3 at N=1: a strided sample of the medium dataset; aggregate GFLOP/s = sum(flops) / sum(kernel time)."""
-    from spmm_amd.datasets import medium_dataset_lines
-    lines = medium_dataset_lines()[args.sample_offset::args.sample_stride]
+def load_pmc_dataset(path: str, k: int, dtype: str) -> dict:
+    """gen line -> per-launch PMC record of THIS engine build, from profiles/pmc_dataset_latest.json ({"records":
+    [...]}, written by tools/pmc_dataset.py publish); {} when none match (the record then carries traffic null)."""
+    p = Path(path)
+    if not p.exists():
+        return {}
+    try:
+        recs = json.loads(p.read_text()).get("records", [])
+    except ValueError:
+        return {}
+    sha = engine_sha256()
+    return {r["gen"]: r for r in recs
+            if r.get("engine_sha256") == sha and r.get("k") == k and r.get("dtype") == dtype}
+
+
+def pctl(v: list, q: float) -> float:
+    s = sorted(v)
+    return s[min(len(s) - 1, int(q * len(s)))] if s else float("nan")
+
+
+def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, cpu_budget_s: float = 0.0,
+              cpu_each_s: float = 0.0, pmc: dict | None = None, names: dict | None = None, log=True) -> dict:
+    """Time every generator line at K (HBM-resident A, B, C; HIP events on the launch stream), self-check sampled
+    rows, attach PMC traffic / the gather ceiling when `pmc` has the line; the CPU baseline runs on the matrices in
+    sample order while `cpu_budget_s` lasts (and `cpu_each_s` per matrix when set: twins).  Matrix generation runs
+    one line ahead on a host thread (the generator releases the GIL), so the GPU does not wait for it."""
+    from concurrent.futures import ThreadPoolExecutor
     dev = torch.device("cuda", 0)
-    K = args.k
-    tdt = torch.float64 if args.dtype == "f64" else torch.float32
-    npdt = np.float64 if args.dtype == "f64" else np.float32
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    npdt = np.float64 if dtype == "f64" else np.float32
+    dt_code = S.F64 if dtype == "f64" else S.F32
     stream = torch.cuda.current_stream(dev)
-    tot_flops = tot_s = tot_bytes = 0.0
-    fracs, bad = [], 0
+    threads, model = cpu_share()
+    pmc = pmc or {}
+    recs, bad = [], 0
+    cpu_left = cpu_budget_s
     t_start = time.perf_counter()
+    ex = ThreadPoolExecutor(max_workers=1)
+    fut = ex.submit(lambda l: S.generate(S.gen_params(l)), lines[0]) if lines else None
     for i, line in enumerate(lines):
-        A = S.generate(S.gen_params(line))
+        A = fut.result()
+        fut = ex.submit(lambda l: S.generate(S.gen_params(l)), lines[i + 1]) if i + 1 < len(lines) else None
         mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdt), A.m, A.ncols, A.nnz, K, 0)
-        x = S.drand48(42, A.ncols * K)
-        Bh = np.ascontiguousarray(x.reshape(K, A.ncols).T).astype(npdt)
-        B = torch.from_numpy(Bh).to(dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(42)
+        B = torch.rand((max(A.ncols, 1), K), generator=g, device=dev, dtype=tdt)
         C = torch.empty((max(A.m, 1), K), device=dev, dtype=tdt)
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, stream.cuda_stream)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
         ev0.record(stream)
-        for _ in range(args.steps):
+        for _ in range(iters):
             mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, stream.cuda_stream)
         ev1.record(stream)
         torch.cuda.synchronize()
-        t = ev0.elapsed_time(ev1) / args.steps * 1e-3
-        chk = selfcheck(A, Bh, C, K, npdt, nsample=32)
+        t = ev0.elapsed_time(ev1) / iters * 1e-3
+        chk = selfcheck(A, lambda cols: B[torch.from_numpy(cols).to(dev)].cpu().numpy(), C, K, npdt, nsample=32)
         bad += 0 if chk["ok"] else 1
-        b = S.bytes_alg(A.m, A.ncols, A.nnz, K, S.F64 if args.dtype == "f64" else S.F32)
-        tot_flops += 2.0 * A.nnz * K
-        tot_s += t
-        tot_bytes += b
-        fracs.append(b / t / 1e9 / HBM_PEAK_GBS)
+        b = S.bytes_alg(A.m, A.ncols, A.nnz, K, dt_code)
+        rec = {"gen": line, "m": int(A.m), "nnz": int(A.nnz), "ms": t * 1e3, "flops": 2.0 * A.nnz * K,
+               "bytes_alg": b, "frac": b / t / 1e9 / HBM_PEAK_GBS, "gflops": 2.0 * A.nnz * K / t / 1e9,
+               "tiles": int(mf.info()[19]), "selfcheck_ok": chk["ok"]}
+        if names:
+            rec["name"] = names.get(line)
+        pm = pmc.get(line)
+        if pm and pm.get("nnz") == A.nnz:
+            rec["traffic"] = pm["traffic_bytes"]
+            ach = achievable(t * 1e3, pm["traffic_bytes"], pm.get("tcc_req"), float(A.ncols) * K * (8 if dtype == "f64" else 4))
+            rec["frac_of_achievable"] = ach["frac_of_achievable"] if ach else None
+        if (cpu_left > 0 or cpu_each_s > 0) and A.nnz > 0:
+            t0 = time.perf_counter()
+            x_col = np.ascontiguousarray(B.t().cpu().numpy()).ravel()[: A.ncols * K]
+            tc = cpu_time_once(A, x_col, K, npdt, threads, cpu_each_s if cpu_each_s > 0 else min(cpu_left, 2.0))
+            rec["cpu_ms"] = tc * 1e3
+            cpu_left -= time.perf_counter() - t0
+            del x_col
+        recs.append(rec)
         mf.close()
-        del B, C
-        print(f"[{i + 1}/{len(lines)}] {line}: {2.0 * A.nnz * K / t / 1e9:.1f} GFLOP/s frac {fracs[-1]:.3f}",
-              file=sys.stderr, flush=True)
-    elapsed = time.perf_counter() - t_start
-    fr = sorted(fracs)
-    line = {
-        "metric": METRIC, "value": round(tot_flops / tot_s / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tot_s / len(lines) * 1e3, 5),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-        "data": "synthetic (own generator, seeded; A values U[0.5,1.5), B drand48(42))",
-        "config": {"workload": f"medium-sample: every {args.sample_stride}th line of synthetic_matrices_medium_dataset "
-                               f"from {args.sample_offset} ({len(lines)} matrices), K={K}", "k": K,
-                   "parallelism": "single-gpu"},
-        "hbm_gbs_alg": round(tot_bytes / tot_s / 1e9, 2),
-        "roofline": {"bound": "hbm", "achieved": round(tot_bytes / tot_s / 1e9, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(tot_bytes / tot_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                     "median_frac": round(fr[len(fr) // 2], 4), "p10_frac": round(fr[len(fr) // 10], 4),
-                     "p90_frac": round(fr[(9 * len(fr)) // 10], 4)},
-        "cpu_baseline": None,
-        "setup": {"wall_s": round(elapsed, 1), "selfcheck_failures": bad},
-    }
+        del B, C, A
+        if log:
+            print(f"[{i + 1}/{len(lines)}] {line}: {rec['gflops']:.1f} GFLOP/s frac {rec['frac']:.3f}"
+                  + (f" cpu {rec['cpu_ms']:.1f} ms" if "cpu_ms" in rec else ""), file=sys.stderr, flush=True)
+    ex.shutdown()
+    return {"recs": recs, "bad": bad, "wall_s": time.perf_counter() - t_start, "threads": threads, "model": model}
+
+
+def summarize(res: dict, K: int) -> dict:
+    recs = res["recs"]
+    tot_f = sum(r["flops"] for r in recs)
+    tot_s = sum(r["ms"] for r in recs) * 1e-3
+    tot_b = sum(r["bytes_alg"] for r in recs)
+    fr = [r["frac"] for r in recs]
+    out = {"matrices": len(recs), "value": round(tot_f / tot_s / 1e9, 3), "unit": "GFLOP/s",
+           "median_gflops": round(pctl([r["gflops"] for r in recs], 0.5), 2),
+           "roofline": {"bound": "hbm", "achieved": round(tot_b / tot_s / 1e9, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(tot_b / tot_s / 1e9 / HBM_PEAK_GBS, 4),
+                        "median_frac": round(pctl(fr, 0.5), 4), "p10_frac": round(pctl(fr, 0.1), 4),
+                        "p90_frac": round(pctl(fr, 0.9), 4)},
+           "mean_ms_per_matrix": round(tot_s * 1e3 / max(len(recs), 1), 5),
+           "selfcheck_failures": res["bad"], "wall_s": round(res["wall_s"], 1)}
+    with_t = [r for r in recs if "traffic" in r]
+    if with_t:
+        tt = sum(r["traffic"] for r in with_t)
+        ts = sum(r["ms"] for r in with_t) * 1e-3
+        fa = [r["frac_of_achievable"] for r in with_t if r.get("frac_of_achievable")]
+        out["roofline"]["traffic"] = tt / len(with_t)
+        out["roofline"]["traffic_note"] = (f"mean PMC past-L2 bytes per launch over the {len(with_t)} matrices with "
+                                           "records for this engine build (profiles/pmc_dataset_latest.json)")
+        out["roofline"]["traffic_gbs_aggregate"] = round(tt / ts / 1e9, 1)
+        out["roofline"]["achievable"] = {"median_frac_of_achievable": round(pctl(fa, 0.5), 4) if fa else None,
+                                         "p10": round(pctl(fa, 0.1), 4) if fa else None,
+                                         "p90": round(pctl(fa, 0.9), 4) if fa else None, "matrices": len(fa)}
+    else:
+        out["roofline"]["traffic"] = None
+        out["roofline"]["achievable"] = None
+    cp = [r for r in recs if "cpu_ms" in r]
+    if cp:
+        cf = sum(r["flops"] for r in cp)
+        cs = sum(r["cpu_ms"] for r in cp) * 1e-3
+        gs = sum(r["ms"] for r in cp) * 1e-3
+        out["cpu_baseline"] = {
+            "value": round(cf / cs / 1e9, 3), "unit": "GFLOP/s", "cores": res["threads"], "kind": "port",
+            "sample": (f"{len(cp)} of the {len(recs)} matrices (in sample order, time-bounded), same A and B as the GPU "
+                       f"run; oracle/liboracle.so (C restatement of compute_csr, bit-identical to the reference build), "
+                       f"{res['threads']} OpenMP threads on {res['model']}; 1 warm-up + median of timed calls each; "
+                       f"aggregate = sum flops / sum time; GPU aggregate on the same subset "
+                       f"{cf / gs / 1e9:.1f} GFLOP/s")}
+    else:
+        out["cpu_baseline"] = None
+    return out
+
+
+def run_dataset_record(args, torch, S, np) -> dict:
+    from spmm_amd.datasets import medium_dataset_lines
+    lines = medium_dataset_lines()[args.dataset_offset::args.dataset_stride]
+    pmc = load_pmc_dataset(args.pmc_dataset, args.k, args.dtype)
+    res = run_lines(lines, args.k, args.dtype, args.dataset_iters, args.dataset_warmup, torch, S, np,
+                    cpu_budget_s=0.0 if args.no_cpu_baseline else args.dataset_cpu_seconds, pmc=pmc)
+    rec = summarize(res, args.k)
+    rec.update({"metric": METRIC, "scaling": "single-gpu", "dtype": args.dtype,
+                "workload": f"every {args.dataset_stride}th line of synthetic_matrices_medium_dataset from "
+                            f"{args.dataset_offset} ({len(lines)} matrices), K={args.k}",
+                "iters_per_matrix": args.dataset_iters, "warmup_per_matrix": args.dataset_warmup})
+    return rec
+
+
+def run_medium_sample(args, torch, S, np):
+    """config 3 at N=1: a strided sample of the medium dataset as the line itself."""
+    torch.cuda.set_device(0)
+    d = run_dataset_record(args, torch, S, np)
+    line = {"metric": METRIC, "value": d["value"], "unit": "GFLOP/s", "n_gpus": 1, "steps": args.dataset_iters,
+            "warmup": args.dataset_warmup, "ms_per_step": d["mean_ms_per_matrix"],
+            "higher_is_better": True, "scaling": "single-gpu", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (own generator, seeded; A values U[0.5,1.5), B torch.rand(seed 42))",
+            "config": {"workload": "medium-sample: " + d["workload"], "k": args.k, "parallelism": "single-gpu"},
+            "roofline": d["roofline"], "cpu_baseline": d["cpu_baseline"],
+            "setup": {"wall_s": d["wall_s"], "selfcheck_failures": d["selfcheck_failures"]}}
+    print(json.dumps(line), flush=True)
+    return 0 if d["selfcheck_failures"] == 0 else 1
+
+
+def run_twins(args, torch, S, np):
+    """config 5: the 52 validation twins (reference config.sh:283-339) at K, fp64 and fp32, one GPU; a CPU baseline
+    on every twin in the same run (oracle compute_csr, time-bounded per twin)."""
+    from spmm_amd.datasets import twins
+    torch.cuda.set_device(0)
+    tw = twins()
+    names = {line: name for name, line in tw.items()}
+    lines = list(tw.values())
+    per = {}
+    bad = 0
+    for dt in ("f64", "f32"):
+        res = run_lines(lines, args.k, dt, args.dataset_iters, args.dataset_warmup, torch, S, np,
+                        cpu_each_s=0.0 if args.no_cpu_baseline else args.twins_cpu_seconds, names=names)
+        s = summarize(res, args.k)
+        s["per_twin"] = [{"name": r["name"], "nnz": r["nnz"], "ms": round(r["ms"], 5), "gflops": round(r["gflops"], 1),
+                          "frac": round(r["frac"], 4), "cpu_gflops": round(r["flops"] / r["cpu_ms"] / 1e6, 2)
+                          if r.get("cpu_ms") else None, "tiles": r["tiles"]} for r in res["recs"]]
+        bad += res["bad"]
+        per[dt] = s
+    line = {"metric": "GFLOP/s, validation twins (config 5), CSR SpMM K=32, aggregate over the twins",
+            "value": per["f64"]["value"], "unit": "GFLOP/s", "n_gpus": 1, "steps": args.dataset_iters,
+            "warmup": args.dataset_warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "single-gpu",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic twins (own generator on the reference's twin lines; A U[0.5,1.5), B torch.rand(42))",
+            "config": {"workload": f"twins: {len(lines)} validation twins (spmm_amd/validation_twins.json), K={args.k}",
+                       "k": args.k, "parallelism": "single-gpu"},
+            "roofline": per["f64"]["roofline"], "cpu_baseline": per["f64"]["cpu_baseline"], "per_dtype": per,
+            "setup": {"selfcheck_failures": bad}}
     print(json.dumps(line), flush=True)
     return 0 if bad == 0 else 1
 
@@ -343,7 +550,7 @@ def run_pipeline(args, torch, S, np):
     line = {
         "metric": "GFLOP/s, sparse-attention pipeline step (SpMM K,Q,V + SDDMM + SpMM), reference formula",
         "value": round(flops / (step_ms * 1e-3) / 1e9, 3), "unit": "GFLOP/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_ms, 5), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(step_ms, 5), "higher_is_better": True, "scaling": "single-gpu",
         "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (DLMC-like random-pruned weights U[-1,1), seeded band+random mask, x drand48(42))",
         "config": {"workload": f"pipeline: m={m} k={k} n={n} weight density {args.pipe_density} mask density "
@@ -355,6 +562,16 @@ def run_pipeline(args, torch, S, np):
     print(json.dumps(line), flush=True)
     pipe.close()
     return 0 if ok else 1
+
+
+def dump_c(path: str, C_all, exact_all, k: int) -> None:
+    """Row sample of C (every 101st row and the last row) + the exact mask of those rows (tests compare runs)."""
+    import numpy as np
+    import torch
+    m = C_all.shape[0]
+    rows = np.unique(np.concatenate([np.arange(0, m, 101), [m - 1]])).astype(np.int64)
+    c = C_all[torch.from_numpy(rows).to(C_all.device)].cpu().numpy()
+    np.savez(path, rows=rows, c=c, exact=np.asarray(exact_all)[rows], k=np.int64(k))
 
 
 def main():
@@ -382,27 +599,27 @@ def main():
     if not torch.cuda.is_available():
         print("error: no HIP device visible (bench.py measures the GPU engine; there is no CPU path)", file=sys.stderr)
         sys.exit(3)
-    if args.workload == "pipeline":
+    single = {"pipeline": run_pipeline, "medium-sample": run_medium_sample, "twins": run_twins}
+    if args.workload in single:
         if N != 1:
-            print("error: --workload pipeline runs on one GPU", file=sys.stderr)
+            print(f"error: --workload {args.workload} runs on one GPU", file=sys.stderr)
             sys.exit(2)
         torch.cuda.set_device(0)
-        if args.dtype == "f64" and "--dtype" not in sys.argv:
+        if args.workload == "pipeline" and args.dtype == "f64" and "--dtype" not in sys.argv:
             args.dtype = "f32"                       # the reference pipeline's configuration
-        sys.exit(run_pipeline(args, torch, S, np))
-    if args.workload == "medium-sample":
-        if N != 1:
-            print("error: --workload medium-sample runs on one GPU", file=sys.stderr)
-            sys.exit(2)
-        torch.cuda.set_device(0)
-        sys.exit(run_medium_sample(args, torch, S, np))
+        sys.exit(single[args.workload](args, torch, S, np))
 
     dist = None
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % ndev if args.dist_backend == "gloo" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if N > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        if args.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend="gloo")
     K = args.k
     tdtype = torch.float64 if args.dtype == "f64" else torch.float32
     npdtype = np.float64 if args.dtype == "f64" else np.float32
@@ -424,7 +641,7 @@ def main():
     ncols = int(p.nr_cols)
 
     t0 = time.perf_counter()
-    mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdtype), A.m, ncols, A.nnz, K, local_rank)
+    mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdtype), A.m, ncols, A.nnz, K, dev_index)
     t_plan = time.perf_counter() - t0
 
     # ---- B: drand48(42) column-major x on rank 0 (the reference harness convention), row-major in HBM, broadcast
@@ -467,56 +684,63 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)   # HIP events on the launch stream
-    kern_all = [kern_ms]
+    elapsed = time.perf_counter() - t0                       # barrier-inclusive wall time of the K steps
+    kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)     # HIP events on the launch stream, per step
+    bytes_launch = S.bytes_alg(A.m, ncols, A.nnz, K, S.F64 if args.dtype == "f64" else S.F32)
+    kern_all, bytes_all = [kern_ms], [bytes_launch]
     if dist is not None:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt[0])
-        kt = torch.zeros(N, device=dev, dtype=torch.float64)
-        kt[rank] = kern_ms
-        dist.all_reduce(kt)
-        kern_all = [float(v) for v in kt.cpu()]
-    kern_max_ms = max(kern_all)
+        kt = sharding.gather_scalars(dist, [kern_ms, bytes_launch, elapsed], dev)
+        kern_all = [v[0] for v in kt]
+        bytes_all = [v[1] for v in kt]
+        elapsed = max(v[2] for v in kt)
+    slow = int(np.argmax(kern_all))
+    kern_max_ms = kern_all[slow]
 
     # ---- C all-gather, once, timed (validation / hand-back path, never inside the timed loop)
     t_gather = None
+    exact = mf.exact_rows()
+    c_all, exact_all = C[: A.m], exact
     if dist is not None:
         counts = [e - s for s, e in bounds]
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
-        c_all = sharding.allgather_rows(dist, C, counts)
+        c_all = sharding.allgather_rows(dist, C[: max(A.m, 1)], counts)
         torch.cuda.synchronize()
         t_gather = time.perf_counter() - tg
-        del c_all
+        ex_t = torch.from_numpy(exact.astype(np.uint8).reshape(-1, 1)).to(dev)
+        exact_all = sharding.allgather_rows(dist, ex_t if A.m else torch.zeros((1, 1), dtype=torch.uint8, device=dev),
+                                            counts).cpu().numpy().ravel().astype(bool)
+    if rank == 0 and args.dump_c:
+        dump_c(args.dump_c, c_all, exact_all, K)
+    del c_all
 
     # ---- self-check on every rank (B rows for the check: rank 0 has them on the host; others copy from HBM)
     Bh_chk = Bh if rank == 0 else B.cpu().numpy()
     chk = selfcheck(A, Bh_chk, C, K, npdtype)
     ok_local = chk["ok"]
     if dist is not None:
-        okt = torch.tensor([0 if ok_local else 1], device=dev, dtype=torch.int32)
-        dist.all_reduce(okt)
-        ok_all = int(okt[0]) == 0
+        ok_all = all(v[0] == 0 for v in sharding.gather_scalars(dist, [0.0 if ok_local else 1.0], dev))
     else:
         ok_all = ok_local
 
     flops_step = 2.0 * nnz_total * K
-    gflops = flops_step * args.steps / elapsed / 1e9
-    s = 8 if args.dtype == "f64" else 4
-    dt_code = S.F64 if s == 8 else S.F32
-    bytes_launch = S.bytes_alg(A.m, ncols, A.nnz, K, dt_code)      # one definition at every N (rank's rows, all cols)
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    gflops = flops_step / (kern_max_ms * 1e-3) / 1e9
+    # the slowest rank bounds the step: its bytes over its time (one definition at every N: the rank's rows and
+    # nonzeros with the global column count)
+    achieved = bytes_all[slow] / (kern_max_ms * 1e-3) / 1e9
+    traffic = l2_req = None
     try:
         pm = json.loads(Path(args.pmc_json).read_text())
         if (pm.get("workload") == gen and pm.get("k") == K and pm.get("dtype") == args.dtype and N == 1
                 and pm.get("nnz") == A.nnz and pm.get("engine_sha256") == engine_sha256()):
             traffic = pm.get("hbm_bytes_per_launch")
+            cc = pm.get("counters_per_launch", {})
+            if "TCC_HIT_sum" in cc and "TCC_MISS_sum" in cc:
+                l2_req = cc["TCC_HIT_sum"] + cc["TCC_MISS_sum"]
     except Exception:
         pass
+    ach = achievable(kern_max_ms, traffic, l2_req, float(ncols) * K * (8 if args.dtype == "f64" else 4))
 
     # ---- plugin end to end (N=1): host x / y through the reference contract (H2D + transpose + kernel + D2H)
     e2e = None
@@ -542,6 +766,14 @@ def main():
             cpu = cpu_baseline(A, x_col, K, args.cpu_warmup, args.cpu_seconds, npdtype)
         except Exception as e:  # the baseline is reported, never required
             cpu = {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
+    mf.close()
+    del B, C
+
+    dataset = None
+    dataset_ok = True
+    if rank == 0 and N == 1 and args.workload == "config2" and not args.no_dataset and args.gen is None:
+        dataset = run_dataset_record(args, torch, S, np)
+        dataset_ok = dataset["selfcheck_failures"] == 0
 
     if rank == 0:
         line = {
@@ -551,7 +783,7 @@ def main():
             "n_gpus": N,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "ms_per_step": round(kern_max_ms, 5),
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
@@ -562,25 +794,29 @@ def main():
                                    + f", K={K}",
                        "nnz_total": nnz_total, "rows_total": int(p.nr_rows), "cols": ncols, "k": K,
                        "nnz_per_rank": per_rank, "imbalance_max_over_mean": round(imbalance, 4),
-                       "parallelism": f"row-shard{N}" if N > 1 else "single-gpu"},
+                       "parallelism": f"row-shard{N}" if N > 1 else "single-gpu",
+                       "dist_backend": args.dist_backend if N > 1 else None},
+            "timing": "value = 2*nnz*K / (max over ranks of the HIP-event time per step of the K timed steps, launch "
+                      "stream); wall_ms_per_step = barrier-inclusive host wall time, max over ranks",
+            "wall_ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "hbm_gbs_alg": round(achieved, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_gbs": None if traffic is None else round(traffic / (kern_ms * 1e-3) / 1e9, 1),
-                         "bytes_alg_per_launch": bytes_launch, "kernel_ms_per_launch": round(kern_ms, 5),
-                         "kernel_ms_per_rank": [round(v, 5) for v in kern_all],
-                         "kernel_ms_max_over_ranks": round(kern_max_ms, 5)},
+                         "traffic_gbs": None if traffic is None else round(traffic / (kern_max_ms * 1e-3) / 1e9, 1),
+                         "achievable": ach,
+                         "bytes_alg_per_launch": bytes_all[slow], "kernel_ms_per_launch": round(kern_max_ms, 5),
+                         "kernel_ms_per_rank": [round(v, 5) for v in kern_all], "slowest_rank": slow},
             "cpu_baseline": cpu,
             "plugin_e2e": e2e,
+            "dataset": dataset,
             "setup": {"gen_s": round(t_gen, 2), "plan_s": round(t_plan, 2), "bcast_B_s": round(t_bcast, 4),
                       "allgather_C_s": None if t_gather is None else round(t_gather, 4),
                       "selfcheck": chk, "selfcheck_all_ranks_ok": ok_all},
         }
         print(json.dumps(line), flush=True)
-    mf.close()
     if dist is not None:
         dist.destroy_process_group()
-    if not ok_all:
+    if not ok_all or not dataset_ok:
         print("error: self-check failed (C not finite or outside the normwise bound)", file=sys.stderr)
         sys.exit(1)
 

@@ -121,7 +121,7 @@ int spmm_hip_set_timing(spmm_hip_t *h, int32_t on);
  * (spmv_kernel.h:20,30; spmv_bench.cpp:441-443,474-476).  Appends CSV columns to buf (at most buf_n bytes incl.
  * NUL) and returns the number of characters written (<0 on error).  Columns:
  *   kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,split_rows,seq_max,panels,
- *   windows,device */
+ *   windows,device,ngpus   (roofline_frac per GPU: hbm_gbs_alg / ngpus / 8000) */
 int spmm_hip_stats_labels(char *buf, long buf_n);
 int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n);
 
@@ -161,6 +161,37 @@ int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask);
 int spmm_hip_device_ptrs(spmm_hip_t *h, void **d_b_rowmajor, void **d_c);
 
 int spmm_hip_destroy(spmm_hip_t *h);
+
+/* ---- Multi-GPU handles (`ngpus` in the factory, the multi-GPU fan-out inside run; §8e).
+ * Same factory arguments as spmm_hip_create plus ngpus and the device of every shard (devices = NULL: 0..ngpus-1;
+ * indices may repeat -- every shard on device 0 is the single-GPU test mode).  A's rows are split into ngpus
+ * contiguous nnz-balanced ranges by the reference partitioner (spmm_hip_partition_rows =
+ * loop_partitioner_balance_prefix_sums, lib/parallel_util.h:141-165); each range becomes a single-device handle on
+ * its GPU (own copy of its rows, own inspector plan, stream and buffers).  The handle works with every entry point
+ * above except spmm_hip_run_device_batch and spmm_hip_device_ptrs:
+ *   spmm_hip_run / spmm_hip_run_rowmajor  host x -> root device (shard 0's) -> replicated to every shard (root->peer
+ *       hipMemcpyPeerAsync over xGMI; SPMM_HIP_BCAST=rccl: one RCCL broadcast, distinct devices only) -> every
+ *       shard's SpMM concurrently -> its rows of y copied back; synchronous, y identical in layout to one device.
+ *   spmm_hip_run_device  d_b and d_c on the ROOT device; shard 0 writes its rows of d_c in place, the others are
+ *       copied in (peer copies); stream-ordered on `stream` (shard streams fork/join by events).
+ *   spmm_hip_update_values  host values, scattered to the shards (the device variant only when all shards share
+ *       one device).
+ *   spmm_hip_last_times  out_ms[0] = broadcast + all shards' SpMMs (the multi-GPU kernel span).
+ * Results: every shard is an independent plan over its rows, so a row is computed exactly as a one-device handle
+ * over those same rows computes it; spmm_hip_exact_rows concatenates the shards' masks. */
+#define SPMM_HIP_BCAST_PEER  0   /* B replicated by root -> peer hipMemcpyPeerAsync (default)              */
+#define SPMM_HIP_BCAST_RCCL  1   /* B replicated by one RCCL broadcast (SPMM_HIP_BCAST=rccl at create)     */
+int spmm_hip_create_multi(const int32_t *row_ptr, const int32_t *col_idx, const void *values, int64_t m,
+                          int64_t ncols, int64_t nnz, int32_t k, int32_t dtype, int32_t ngpus, const int32_t *devices,
+                          spmm_hip_t **out);
+/* Shards of a handle (1 for spmm_hip_create handles) and the broadcast mode in use. */
+int spmm_hip_ngpus(const spmm_hip_t *h, int32_t *ngpus, int32_t *bcast_mode);
+/* Shard g: its device, its C rows [*row0, *row1) and its device-local C buffer ([rows][k], row-major). */
+int spmm_hip_shard(const spmm_hip_t *h, int32_t g, int32_t *device, int64_t *row0, int64_t *row1, void **d_c);
+/* The timed multi-GPU path: replicate B (root device, either layout) once, then spmm_hip_run_sharded computes every
+ * shard's rows into its own C buffer (spmm_hip_shard), leaving C sharded -- no gather inside the loop (§8e). */
+int spmm_hip_broadcast_b(spmm_hip_t *h, const void *d_b, int32_t b_layout, int32_t k, void *stream);
+int spmm_hip_run_sharded(spmm_hip_t *h, int32_t k, void *stream);
 
 /* nnz-balanced row split (reference: loop_partitioner_balance_prefix_sums, lib/parallel_util.h:141-165, with
  * binary_search lib/macros/macrolib.h:471-524): worker w of W gets rows [*start, *end).  Used for GPU shards. */

@@ -31,18 +31,21 @@
 #include <vector>
 
 #include "../../include/spmm_hip.h"
+#include "spmm_handle.hpp"
 #include "spmm_kernels.hpp"
 
 using namespace spmm;
+using namespace spmm_engine;
 
-namespace {
-
+namespace spmm_engine {
 thread_local std::string g_detail;
-
 int fail(int status, const std::string &what) {
     g_detail = what;
     return status;
 }
+}  // namespace spmm_engine
+
+namespace {
 
 #define HIPCHK(expr)                                                                                     \
     do {                                                                                                 \
@@ -75,103 +78,6 @@ constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgr
 constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
 constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value +0, the zero B row)
 constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
-
-// Production kernel variant (tools/tune_kernel.py on MI355X).
-#ifndef DEF_U
-#define DEF_U 16
-#endif
-#ifndef DEF_NTC
-#define DEF_NTC 1
-#endif
-#ifndef DEF_DMA
-#define DEF_DMA 0
-#endif
-#ifndef DEF_BUF
-#define DEF_BUF 1
-#endif
-
-
-struct Plan {
-    int k = -1;
-    int kw = 0, npanels = 0;   // panel width (columns) and count
-    int seq_max = 0;           // T
-    int cap = 0;               // block capacity (nonzeros)
-    int64_t win_cols = 0;      // column-window width (0 = one window over all columns)
-    int nwin = 1;              // column windows (one launch each per K panel)
-    int64_t nseg = 0;          // virtual rows (segments) over all windows
-    int xcd = 0;               // 1 = XCD-contiguous block order (each XCD sweeps one eighth of the rows)
-    int lmax = 1;              // vector lanes: max groups per row (1 = every row one group, exact)
-    int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
-    int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
-    int tile_xcd = 0;          // tiles in XCD-contiguous order
-    int tile_wide = 1;         // compute-lane width in 16-byte pieces of a B row (1, 2, 4), where RPG allows
-    int64_t tile_rows = 0, tile_nnz = 0, tile_chunks = 0;
-    double tile_reuse = 0.0;   // sampled mean reuse (nnz per union column) the policy saw
-};
-
-struct Variant {
-    int u = DEF_U, ntc = DEF_NTC, dma = DEF_DMA, buf = DEF_BUF;
-    int seq_max = 0, cap = 0;  // 0 = inspector policy
-    int panel_k = 0;           // 0 = inspector policy
-    int64_t win_bytes = 0;     // 0 = inspector policy, < 0 = no column windows, > 0 = window of this many B bytes
-    int xcd = 0;               // 0 = inspector policy, < 0 = off, > 0 = XCD-contiguous block order
-    int lanes = 0;             // 0 = inspector policy, < 0 = off (exact rows), > 0 = vector lanes up to this many
-    int tiles = 0;             // 0 = inspector policy, < 0 = off, > 0 = every eligible tile with reuse >= 1
-};
-
-}  // namespace
-
-struct spmm_hip_handle {
-    int device = 0;
-    int dtype = SPMM_HIP_F64;
-    size_t vsize = 8;
-    int64_t m = 0, ncols = 0, nnz = 0;
-    std::vector<int32_t> h_row_ptr;  // kept for re-inspection at plan time
-
-    int32_t *d_col = nullptr;
-    void *d_val = nullptr;
-
-    // inspector output (per plan)
-    Plan plan;
-    Variant var;
-    int64_t nv = 0;                  // virtual rows
-    int nblk = 0, nlong = 0, nslots = 0;
-    int32_t *d_vrow_ptr = nullptr, *d_vdest = nullptr;
-    int4 *d_blk = nullptr;           // {first, end | flags, vrow_ptr[first], vrow_ptr[end]} per block
-    int4 *d_long_rows = nullptr;
-    std::vector<int> win_blk;        // blocks of column window w: [win_blk[w], win_blk[w+1])
-    std::vector<int64_t> win_v;      // virtual rows of column window w: [win_v[w], win_v[w+1])
-    std::vector<uint8_t> exact;      // per C row: 1 = one left-to-right FMA chain (spmm_hip_exact_rows)
-    int32_t *d_lr_cnt = nullptr;     // fused combine: per split row, pieces stored so far in this launch (re-armed to 0)
-    int32_t *d_slot_lr = nullptr;    // fused combine: partial slot -> split row
-    bool fuse = false;               // split rows combined inside the row kernel (no spmm_combine_kernel launch)
-    int32_t *d_wcol = nullptr;       // chained mode: col_idx / values in window-major segment order
-    void *d_wval = nullptr;
-    int4 *d_tiles = nullptr, *d_tchunk = nullptr;   // tile mode (spmm_tile_kernel)
-    int32_t *d_tcol = nullptr;
-    uint16_t *d_tseg = nullptr, *d_tlidx = nullptr;
-    void *d_tval = nullptr;
-    long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
-    int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)
-    int32_t *d_tperm = nullptr;      // tile chunk-major position -> nonzero, -1 = padding (value updates re-gather tval)
-    int64_t nwperm = 0, ntperm = 0;
-
-    // per-k buffers
-    void *d_b = nullptr;      // row-major B [ncols][k]
-    void *d_xcol = nullptr;   // column-major staging for host uploads / device col-major input
-    void *d_c = nullptr;      // row-major C [m][k]
-    void *d_part = nullptr;   // split-row partials [nslots][k]
-    size_t b_bytes = 0, c_bytes = 0, insp_bytes = 0;
-
-    const void *last_x = nullptr;
-    hipStream_t stream = nullptr;  // own stream for spmm_hip_run
-    hipEvent_t ev[8] = {};
-    bool have_times = false, have_transpose = false, have_copies = false;
-    bool rec_events = false;         // run_device records timing events (spmm_hip_set_timing / SPMM_HIP_EVENTS=1)
-    int64_t a_bytes = 0;
-};
-
-namespace {
 
 int pow2_ceil(int64_t x) {
     int p = 1;
@@ -395,6 +301,9 @@ int launch_spmm(spmm_hip_t *h, const void *B, void *C, int K, hipStream_t s) {
     return SPMM_HIP_OK;
 }
 
+}  // namespace
+
+namespace spmm_engine {
 int launch_transpose(spmm_hip_t *h, const void *X, void *Bt, int K, hipStream_t s) {
     if (h->ncols == 0 || K == 0) return SPMM_HIP_OK;
     dim3 grid((unsigned)((h->ncols + 63) / 64), (unsigned)((K + 31) / 32));
@@ -406,6 +315,9 @@ int launch_transpose(spmm_hip_t *h, const void *X, void *Bt, int K, hipStream_t 
     if (e != hipSuccess) return fail(SPMM_HIP_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(e));
     return SPMM_HIP_OK;
 }
+}  // namespace spmm_engine
+
+namespace {
 
 // ------------------------------------------------------------------------------------------------- inspector
 // Split length T.  A row is one serial chain of len/U dependent gather batches; measured on MI355X (§6.2) a chain
@@ -1116,6 +1028,7 @@ int spmm_hip_create(const int32_t *row_ptr, const int32_t *col_idx, const void *
 int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     if (!h || k < 1) return fail(SPMM_HIP_ERR_ARG, "plan: bad handle or k < 1");
     if (h->plan.k == k) return SPMM_HIP_OK;
+    if (h->multi) return multi_plan(h, k);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     free_plan(h);
@@ -1442,6 +1355,7 @@ int spmm_hip_run_device(spmm_hip_t *h, const void *d_b, int32_t b_layout, void *
     }
     if (((uintptr_t)d_b | (uintptr_t)d_c) % 16 != 0)
         return fail(SPMM_HIP_ERR_ARG, "run_device: device buffers must be 16-byte aligned");
+    if (h->multi) return multi_run_device(h, d_b, b_layout, d_c, k, (hipStream_t)stream);
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
     const void *B = d_b;
@@ -1489,6 +1403,7 @@ int spmm_hip_run_device_batch(int32_t count, spmm_hip_t *const *hs, const void *
     if (count < 1 || !hs || !d_b || !b_layout || !d_c || !k) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: bad arguments");
     for (int i = 0; i < count; ++i) {
         if (!hs[i]) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: null handle");
+        if (hs[i]->multi) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: multi-GPU handles fan out on their own");
         if (hs[i]->device != hs[0]->device) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: handles on different devices");
         for (int j = 0; j < i; ++j)
             if (hs[j] == hs[i]) return fail(SPMM_HIP_ERR_ARG, "run_device_batch: a handle appears twice");
@@ -1580,12 +1495,14 @@ extern "C" {
 
 int spmm_hip_update_values_device(spmm_hip_t *h, const void *d_vals, void *stream) {
     if (!h || (!d_vals && h->nnz > 0)) return fail(SPMM_HIP_ERR_ARG, "update_values_device: bad arguments");
+    if (h->multi) return multi_update_values(h, d_vals, true, (hipStream_t)stream);
     HIPCHK(hipSetDevice(h->device));
     return update_values(h, d_vals, hipMemcpyDeviceToDevice, (hipStream_t)stream);
 }
 
 int spmm_hip_update_values(spmm_hip_t *h, const void *vals) {
     if (!h || (!vals && h->nnz > 0)) return fail(SPMM_HIP_ERR_ARG, "update_values: bad arguments");
+    if (h->multi) return multi_update_values(h, vals, false, nullptr);
     HIPCHK(hipSetDevice(h->device));
     int st = update_values(h, vals, hipMemcpyHostToDevice, h->stream);
     if (st != SPMM_HIP_OK) return st;
@@ -1597,6 +1514,7 @@ int spmm_hip_update_values(spmm_hip_t *h, const void *vals) {
 // pipeline_code_bench/sddmm_taco_naive.cpp:219-249): upload straight into the engine's B, no transpose.
 int spmm_hip_run_rowmajor(spmm_hip_t *h, const void *x, void *y, int32_t k) {
     if (!h || k < 1 || (!x && h->ncols > 0) || (!y && h->m > 0)) return fail(SPMM_HIP_ERR_ARG, "run_rowmajor: bad arguments");
+    if (h->multi) return multi_run_host(h, x, y, k, true);
     if (h->plan.k != k) {
         int st = spmm_hip_plan(h, k);
         if (st != SPMM_HIP_OK) return st;
@@ -1623,6 +1541,7 @@ int spmm_hip_run_rowmajor(spmm_hip_t *h, const void *x, void *y, int32_t k) {
 
 int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k) {
     if (!h || k < 1 || (!x && h->ncols > 0) || (!y && h->m > 0)) return fail(SPMM_HIP_ERR_ARG, "run: bad arguments");
+    if (h->multi) return multi_run_host(h, x, y, k, false);
     if (h->plan.k != k) {
         int st = spmm_hip_plan(h, k);
         if (st != SPMM_HIP_OK) return st;
@@ -1663,6 +1582,7 @@ int spmm_hip_set_timing(spmm_hip_t *h, int32_t on) {
 
 int spmm_hip_last_times(spmm_hip_t *h, double *out_ms) {
     if (!h || !out_ms) return fail(SPMM_HIP_ERR_ARG, "last_times: bad arguments");
+    if (h->multi) return multi_last_times(h, out_ms);
     for (int i = 0; i < 4; ++i) out_ms[i] = 0.0;
     if (!h->have_times) return SPMM_HIP_OK;
     float ms = 0.f;
@@ -1687,7 +1607,7 @@ int spmm_hip_stats_labels(char *buf, long buf_n) {
     if (!buf || buf_n <= 0) return fail(SPMM_HIP_ERR_ARG, "stats_labels: buffer");
     int n = snprintf(buf, (size_t)buf_n,
                      ",kernel_ms,transpose_ms,h2d_ms,d2h_ms,bytes_alg,hbm_gbs_alg,roofline_frac,blocks,split_rows,"
-                     "seq_max,panels,windows,device");
+                     "seq_max,panels,windows,device,ngpus");
     return (int)std::min<long>(n, buf_n - 1);
 }
 
@@ -1699,9 +1619,14 @@ int spmm_hip_stats(spmm_hip_t *h, char *buf, long buf_n) {
     const int k = h->plan.k > 0 ? h->plan.k : 0;
     const double bytes = spmm_hip_bytes_alg(h->m, h->ncols, h->nnz, k, h->dtype);
     const double gbs = t[0] > 0 ? bytes / (t[0] * 1e-3) / 1e9 : 0.0;
-    int n = snprintf(buf, (size_t)buf_n, ",%.6f,%.6f,%.6f,%.6f,%.0f,%.2f,%.4f,%d,%d,%d,%d,%d,%d", t[0], t[1], t[2], t[3],
-                     bytes, gbs, gbs / 8000.0, h->nblk, h->nlong, h->plan.seq_max, h->plan.npanels, h->plan.nwin,
-                     h->device);
+    int64_t inf[SPMM_HIP_INFO_SLOTS];
+    spmm_hip_info(h, inf);
+    int32_t ng = 1;
+    spmm_hip_ngpus(h, &ng, nullptr);
+    // roofline_frac against ONE GPU's 8 TB/s (a multi-GPU handle's rate is the sum over its ngpus GPUs)
+    int n = snprintf(buf, (size_t)buf_n, ",%.6f,%.6f,%.6f,%.6f,%.0f,%.2f,%.4f,%lld,%lld,%d,%d,%d,%d,%d", t[0], t[1],
+                     t[2], t[3], bytes, gbs, gbs / 8000.0 / ng, (long long)inf[5], (long long)inf[6], h->plan.seq_max,
+                     h->plan.npanels, h->plan.nwin, h->device, ng);
     return (int)std::min<long>(n, buf_n - 1);
 }
 
@@ -1728,6 +1653,7 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out) {
     out[17] = h->plan.exact_rows;
     out[18] = h->fuse ? 1 : 0;
     out[19] = h->plan.ntile;
+    if (h->multi) multi_info(h, out);     // blocks, split rows, device bytes, fuse: summed over the shards
     return SPMM_HIP_OK;
 }
 
@@ -1761,6 +1687,7 @@ int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask) {
 
 int spmm_hip_device_ptrs(spmm_hip_t *h, void **d_b_rowmajor, void **d_c) {
     if (!h || h->plan.k < 1) return fail(SPMM_HIP_ERR_ARG, "device_ptrs: handle not planned");
+    if (h->multi) return fail(SPMM_HIP_ERR_ARG, "device_ptrs: a multi-GPU handle has no single C (spmm_hip_shard)");
     if (d_b_rowmajor) *d_b_rowmajor = h->d_b;
     if (d_c) *d_c = h->d_c;
     return SPMM_HIP_OK;
@@ -1768,6 +1695,7 @@ int spmm_hip_device_ptrs(spmm_hip_t *h, void **d_b_rowmajor, void **d_c) {
 
 int spmm_hip_destroy(spmm_hip_t *h) {
     if (!h) return SPMM_HIP_OK;
+    multi_destroy(h);
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_plan(h);

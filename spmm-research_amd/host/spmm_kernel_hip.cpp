@@ -7,7 +7,9 @@
 //
 // Environment:
 //   SPMM_HIP_DEVICE              device index (default 0)
+//   SPMM_HIP_NGPUS, SPMM_HIP_DEVICES  multi-GPU handle: rows split over NGPUS GPUs (listed, default 0..NGPUS-1)
 //   SPMM_HIP_ASSUME_X_UNCHANGED  1 = skip re-uploading B when the same x pointer comes back (see spmm_hip.h)
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -59,7 +61,27 @@ struct Matrix_Format *csr_to_format(INT_T *row_ptr, INT_T *col_ind, ValueType *v
     csr->ja = col_ind;
     csr->a = values;
     const char *dev = getenv("SPMM_HIP_DEVICE");
-    int st = spmm_hip_create(row_ptr, col_ind, values, m, n, nnz, k, kDtype, dev ? atoi(dev) : 0, &csr->h);
+    const char *ng = getenv("SPMM_HIP_NGPUS");
+    const char *devs = getenv("SPMM_HIP_DEVICES");
+    int st;
+    if (ng && atoi(ng) > 1) {   // multi-GPU handle (SURVEY §8b ngpus); SPMM_HIP_DEVICES=d0,d1,... (repeats allowed)
+        const int g = std::min(atoi(ng), 64);
+        int32_t dl[64];
+        int nd = 0;
+        for (const char *p = devs; p && *p && nd < 64;) {
+            char *e = nullptr;
+            dl[nd++] = (int32_t)strtol(p, &e, 10);
+            p = (*e == ',') ? e + 1 : e;
+            if (e && *e != ',') break;
+        }
+        if (devs && nd != g) {
+            fprintf(stderr, "HIP_CSR_MI355X: SPMM_HIP_DEVICES lists %d devices, SPMM_HIP_NGPUS=%d\n", nd, g);
+            exit(EXIT_FAILURE);
+        }
+        st = spmm_hip_create_multi(row_ptr, col_ind, values, m, n, nnz, k, kDtype, g, devs ? dl : nullptr, &csr->h);
+    } else {
+        st = spmm_hip_create(row_ptr, col_ind, values, m, n, nnz, k, kDtype, dev ? atoi(dev) : 0, &csr->h);
+    }
     if (st != SPMM_HIP_OK) die("csr_to_format", st);
     int64_t info[SPMM_HIP_INFO_SLOTS];
     spmm_hip_info(csr->h, info);

@@ -103,6 +103,11 @@ class _Tiles(C.Structure):
 def _bind_hip(L: C.CDLL) -> C.CDLL:
     vp, i32, i64 = C.c_void_p, C.c_int32, _i64
     L.spmm_hip_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)]
+    L.spmm_hip_create_multi.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, vp, C.POINTER(vp)]
+    L.spmm_hip_ngpus.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
+    L.spmm_hip_shard.argtypes = [vp, i32, C.POINTER(i32), C.POINTER(i64), C.POINTER(i64), C.POINTER(vp)]
+    L.spmm_hip_broadcast_b.argtypes = [vp, vp, i32, i32, vp]
+    L.spmm_hip_run_sharded.argtypes = [vp, i32, vp]
     L.spmm_hip_run.argtypes = [vp, vp, vp, i32]
     L.spmm_hip_run_device.argtypes = [vp, vp, i32, vp, i32, vp]
     L.spmm_hip_run_device_batch.argtypes = [i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32), C.POINTER(vp),
@@ -380,7 +385,8 @@ class MatrixFormat:
 
     format_name = "HIP_CSR_MI355X"
 
-    def __init__(self, row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0):
+    def __init__(self, row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0,
+                 ngpus: int = 1, devices=None):
         self.m, self.n, self.nnz = int(m), int(n), int(nnz)
         vals = np.ascontiguousarray(values)
         if vals.dtype not in (np.float64, np.float32):
@@ -393,8 +399,15 @@ class MatrixFormat:
             ci = np.zeros(1, np.int32)
             vals = np.zeros(1, self.dtype)
         self._h = C.c_void_p()
-        _check("csr_to_format", hip.spmm_hip_create(rp, ci, vals.ctypes.data_as(C.c_void_p), self.m, self.n,
-                                                    self.nnz, int(k), self._dt, int(device), C.byref(self._h)))
+        if ngpus > 1 or devices is not None:
+            # multi-GPU handle (spmm_hip_create_multi): nnz-balanced row shards, one per device
+            ng = int(ngpus if devices is None else len(devices))
+            devs = None if devices is None else (C.c_int32 * ng)(*[int(d) for d in devices])
+            _check("csr_to_format", hip.spmm_hip_create_multi(rp, ci, vals.ctypes.data_as(C.c_void_p), self.m, self.n,
+                                                              self.nnz, int(k), self._dt, ng, devs, C.byref(self._h)))
+        else:
+            _check("csr_to_format", hip.spmm_hip_create(rp, ci, vals.ctypes.data_as(C.c_void_p), self.m, self.n,
+                                                        self.nnz, int(k), self._dt, int(device), C.byref(self._h)))
         self.csr_mem_footprint = self.nnz * (self.dtype.itemsize + 4) + (self.m + 1) * 4
         self.mem_footprint = float(self.info()[7])
 
@@ -430,6 +443,24 @@ class MatrixFormat:
         """HBM-resident run: d_b / d_c are device addresses (e.g. torch tensor .data_ptr())."""
         _check("spmm_device", hip.spmm_hip_run_device(self._h, C.c_void_p(d_b), b_layout, C.c_void_p(d_c), k,
                                                       C.c_void_p(stream)))
+
+    def ngpus(self) -> tuple[int, int]:
+        """(shards, broadcast mode: 0 peer copies, 1 RCCL)."""
+        n, b = C.c_int32(), C.c_int32()
+        _check("ngpus", hip.spmm_hip_ngpus(self._h, C.byref(n), C.byref(b)))
+        return n.value, b.value
+
+    def shard(self, g: int) -> dict:
+        """Shard g of the handle: device, C rows [row0, row1), device-local C buffer address."""
+        d, r0, r1, c = C.c_int32(), _i64(), _i64(), C.c_void_p()
+        _check("shard", hip.spmm_hip_shard(self._h, g, C.byref(d), C.byref(r0), C.byref(r1), C.byref(c)))
+        return {"device": d.value, "row0": r0.value, "row1": r1.value, "d_c": c.value or 0}
+
+    def broadcast_b(self, d_b: int, b_layout: int, k: int, stream: int = 0) -> None:
+        _check("broadcast_b", hip.spmm_hip_broadcast_b(self._h, C.c_void_p(d_b), b_layout, k, C.c_void_p(stream)))
+
+    def run_sharded(self, k: int, stream: int = 0) -> None:
+        _check("run_sharded", hip.spmm_hip_run_sharded(self._h, k, C.c_void_p(stream)))
 
     def plan(self, k: int) -> None:
         _check("plan", hip.spmm_hip_plan(self._h, k))
@@ -498,9 +529,10 @@ def run_device_batch(entries, stream: int = 0) -> None:
     _check("run_device_batch", hip.spmm_hip_run_device_batch(n, hs, bs, lay, cs, ks, C.c_void_p(stream)))
 
 
-def csr_to_format(row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0) -> MatrixFormat:
-    """Factory with the reference's signature (spmv_kernel.h:29)."""
-    return MatrixFormat(row_ptr, col_ind, values, m, n, nnz, k, device)
+def csr_to_format(row_ptr, col_ind, values, m: int, n: int, nnz: int, k: int = 0, device: int = 0, ngpus: int = 1,
+                  devices=None) -> MatrixFormat:
+    """Factory with the reference's signature (spmv_kernel.h:29); ngpus / devices: a multi-GPU handle."""
+    return MatrixFormat(row_ptr, col_ind, values, m, n, nnz, k, device, ngpus, devices)
 
 
 def statistics_print_labels() -> str:

@@ -63,8 +63,18 @@ def shard_bounds(params, world: int) -> list[tuple[int, int]]:
     return [partition_rows(rp, nnz, world, w) for w in range(world)]
 
 
+def _host_staged(dist, t) -> bool:
+    """gloo (the CPU / shared-GPU test backend) runs the collectives below on host copies of device tensors."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
 def broadcast_b(dist, b, src: int = 0) -> None:
     """Replicate B (any torch tensor on the group's device) from `src` -- one collective, setup only."""
+    if _host_staged(dist, b):
+        h = b.cpu()
+        dist.broadcast(h, src=src)
+        b.copy_(h)
+        return
     dist.broadcast(b, src=src)
 
 
@@ -74,11 +84,26 @@ def allgather_rows(dist, c_local, counts: list[int]):
     world = len(counts)
     mx = max(counts) if counts else 0
     k = c_local.shape[1]
-    pad = torch.zeros((mx, k), dtype=c_local.dtype, device=c_local.device)
-    pad[: c_local.shape[0]] = c_local[: counts[dist.get_rank()]]
+    staged = _host_staged(dist, c_local)
+    dev = torch.device("cpu") if staged else c_local.device
+    pad = torch.zeros((max(mx, 1), k), dtype=c_local.dtype, device=dev)
+    n = counts[dist.get_rank()]
+    pad[:n] = c_local[:n].to(dev)
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad)
-    return torch.cat([bufs[w][: counts[w]] for w in range(world)], dim=0)
+    out = torch.cat([bufs[w][: counts[w]] for w in range(world)], dim=0)
+    return out.to(c_local.device) if staged else out
+
+
+def gather_scalars(dist, vals: list[float], device) -> list[list[float]]:
+    """Every rank's small vector of floats, on every rank (timings, byte counts, flags): [rank][i]."""
+    import torch
+    world = dist.get_world_size()
+    dev = torch.device("cpu") if dist.get_backend() == "gloo" else device
+    t = torch.zeros((world, len(vals)), dtype=torch.float64, device=dev)
+    t[dist.get_rank()] = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return t.cpu().tolist()
 
 
 def imbalance(params, world: int) -> float:

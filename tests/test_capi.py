@@ -59,3 +59,27 @@ def test_single_hip_runtime_in_process():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "1"
+
+
+def test_multi_gpu_factory_fails_loudly_without_gpu():
+    """spmm_hip_create_multi validates its arguments, then needs devices: no CPU fallback."""
+    import numpy as np
+    import spmm_amd as S
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is visible: tests/test_gpu_multi.py covers the multi-GPU handle")
+    except ImportError:
+        pass
+    rp = np.array([0, 1, 2], np.int32)
+    ci = np.array([0, 1], np.int32)
+    va = np.ones(2)
+    with pytest.raises(S.SpmmHipError) as e:
+        S.csr_to_format(rp, ci, va, 2, 2, 2, 4, ngpus=2)
+    assert e.value.status == -4                              # no HIP device
+    h = ctypes.c_void_p()
+    assert S.hip.spmm_hip_create_multi(rp, ci, va.ctypes.data_as(ctypes.c_void_p), 2, 2, 2, 4, 0, 0, None,
+                                       ctypes.byref(h)) == -1        # ngpus < 1
+    bad = np.array([0, 2, 1], np.int32)
+    assert S.hip.spmm_hip_create_multi(bad, ci, va.ctypes.data_as(ctypes.c_void_p), 2, 2, 1, 4, 0, 2, None,
+                                       ctypes.byref(h)) == -6        # malformed CSR (before any device work)

@@ -53,6 +53,9 @@ def _worker(rank, world, port, outdir, gen, mode):
     counts = [e - s for s, e in sharding.shard_bounds(p, world)]
     assert counts[rank] == sh.r1 - sh.r0
     c_all = sharding.allgather_rows(dist, torch.from_numpy(np.ascontiguousarray(c_local)), counts)
+    # per-rank scalars (bench.py's max-over-ranks kernel time, slowest rank's bytes, self-check flags)
+    sc = sharding.gather_scalars(dist, [float(rank), float(counts[rank])], torch.device("cpu"))
+    assert [v[0] for v in sc] == list(range(world)) and [v[1] for v in sc] == [float(c) for c in counts]
     if rank == 0:
         np.save(Path(outdir) / "c_all.npy", c_all.numpy())
         np.save(Path(outdir) / "x_col.npy", x_col)

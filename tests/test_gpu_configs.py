@@ -3,7 +3,8 @@
 * Config 3 (synthetic_matrices_medium_dataset, K in {1, 8, 32, 128}, fp64): one line of every avg class
   {5,10,20,50,100,500} x bw {0.05, 0.6}, drawn with a fixed seed from the dataset's own lines (tools-free restatement
   of its recipe, spmm_amd.datasets), plus the dense-band line 39120 x 500 bw 0.05.
-* Config 5 (validation twins, reference config.sh:283-339): six twins of different character, fp32 AND fp64, K=32.
+* Config 5 (validation twins, reference config.sh:283-339): every twin up to 40 M nonzeros (44 of 53), fp32 AND
+  fp64, K=32.
 * Config 4 (large dataset, gamma rows, nnz-balanced split over 8 GPUs): the 8 shards of the reference partitioner
   (lib/parallel_util.h:141-165) run one after another on this GPU; concatenated they must equal the whole-matrix
   run on every row both runs compute exactly, and a row sample of every shard must match the oracle.  Once in
@@ -60,7 +61,19 @@ def test_config3_medium_lines(env, line):
         assert n_ex + n_in == len(rows)
 
 
-TWINS = ["scircuit", "raefsky3", "cant", "ASIC_680k", "rail4284", "webbase-1M"]
+def twin_names(max_nnz=4.0e7):
+    """Every validation twin up to max_nnz nonzeros (44 of the 53 lines; the 9 larger ones -- up to kmer_V2a's
+    117 M nonzeros -- run in `bench.py --workload twins`)."""
+    from spmm_amd.datasets import twins
+    out = []
+    for name, line in twins().items():
+        f = line.split()
+        if int(f[0]) * float(f[2]) <= max_nnz:
+            out.append(name)
+    return out
+
+
+TWINS = twin_names()
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32], ids=["f64", "f32"])

@@ -1,18 +1,23 @@
 #!/usr/bin/env python3
-"""tools/pmc_dataset.py -- per-matrix HBM traffic (rocprofv3 PMC) over a stratified medium-dataset subset.
+"""tools/pmc_dataset.py -- per-matrix HBM traffic (rocprofv3 PMC) over medium-dataset lines.
 
 BASELINE config 3 asks for "rocprof HBM-BW per matrix".  One driver process (`run`) generates each matrix of the
-subset, plans it at K (fp64), and launches `--launches` SpMMs on HBM-resident B and C; between matrices it launches a
-one-element torch fill, whose dispatch marks the boundary in the profiler's CSV.  `collect` runs that same driver
-under rocprofv3 once per counter group (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass, and
-PMC runs never carry other traces) and once with --kernel-trace for durations, then attributes every engine
-dispatch (spmm_rows_kernel / spmm_tile_kernel / spmm_combine_kernel) to its matrix by marker order.
+set (one line ahead on a host thread), plans it at K, and launches `--launches` SpMMs on HBM-resident B and C;
+between matrices it launches a one-element torch fill, whose dispatch marks the boundary in the profiler's CSV.
+`collect` runs that same driver under rocprofv3 once with --kernel-trace (durations) and once per counter group
+(PMC runs never carry other traces; FETCH_SIZE takes 3 of the 4 TCC counters of a pass, so it runs alone, and
+WRITE_SIZE (2) shares a pass with TCC_HIT_sum + TCC_MISS_sum), then attributes every engine dispatch
+(spmm_rows_kernel / spmm_tile_kernel / spmm_combine_kernel) to its matrix by marker order.
 
 Per matrix and launch (MI355X_MICROARCH.md §HBM): read bytes = 2 x FETCH_SIZE KiB (the gfx950 wide-read correction),
 write bytes = WRITE_SIZE KiB; both sit on the L2 memory side, so Infinity-Cache hits are included (L2-miss traffic,
-an upper bound on true HBM bytes).  Rate = traffic / kernel time (sum of the launch's engine dispatches).
+an upper bound on true HBM bytes).  Rate = traffic / kernel time.  Each record carries the engine build's
+fingerprint (bench.engine_sha256), the L2 requests (TCC_HIT + TCC_MISS) and the gather-ceiling fraction
+(bench.achievable); bench.py reads these records for its dataset sub-record.
 
-  python tools/pmc_dataset.py collect --per-class 6 --k 32 --out profiles/r02_pmc_medium.jsonl
+Sets:  --set stratified --per-class N   N lines of every (avg nnz/row, bw) class, evenly spaced in dataset order
+       --set sample --stride S          every S-th dataset line (bench.py's dataset sub-record: S = 160)
+  python tools/pmc_dataset.py collect --set sample --stride 160 --out gpurun_out/pmc_dataset/sample160.jsonl
 """
 import argparse
 import csv
@@ -27,52 +32,64 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
+sys.path.insert(0, str(ROOT))
 ENGINE = ("spmm_rows_kernel", "spmm_tile_kernel", "spmm_combine_kernel")
-PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]]
+PASSES = [["FETCH_SIZE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]]
 
 
-def subset(per_class, max_nnz):
-    """per_class lines of every (avg nnz/row, bw) class, evenly spaced over the class in dataset order."""
+def lines_for(args):
     from spmm_amd.datasets import medium_dataset_lines
+    L = medium_dataset_lines()
+    if args.set == "sample":
+        return L[args.offset::args.stride]
     cls = defaultdict(list)
-    for line in medium_dataset_lines():
+    for line in L:
         g = line.split()
-        if int(g[0]) * float(g[2]) > max_nnz:
+        if int(g[0]) * float(g[2]) > args.max_nnz:
             continue
         cls[(int(g[2]), float(g[6]))].append(line)
     out = []
     for key in sorted(cls):
-        L = cls[key]
-        idx = np.linspace(0, len(L) - 1, per_class).round().astype(int)
-        out += [L[i] for i in sorted(set(idx))]
+        c = cls[key]
+        idx = np.linspace(0, len(c) - 1, args.per_class).round().astype(int)
+        out += [c[i] for i in sorted(set(idx))]
     return out
 
 
 def run(args):
+    from concurrent.futures import ThreadPoolExecutor
     import torch
     import spmm_amd as S
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
-    lines = subset(args.per_class, args.max_nnz)
+    lines = lines_for(args)
     marker = torch.zeros(1, device=dev)
     manifest = []
-    for line in lines:
-        A = S.generate(S.gen_params(line))
-        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, 0, 0)
+    tdt = torch.float64 if args.dtype == "f64" else torch.float32
+    npdt = np.float64 if args.dtype == "f64" else np.float32
+    ex = ThreadPoolExecutor(max_workers=1)
+    gen = lambda l: S.generate(S.gen_params(l))  # noqa: E731
+    fut = ex.submit(gen, lines[0])
+    for i, line in enumerate(lines):
+        A = fut.result()
+        if i + 1 < len(lines):
+            fut = ex.submit(gen, lines[i + 1])
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdt), A.m, A.ncols, A.nnz, 0, 0)
         mf.plan(args.k)
         g = torch.Generator(device=dev)
         g.manual_seed(42)
-        B = torch.rand((A.ncols, args.k), generator=g, device=dev, dtype=torch.float64)
-        Cm = torch.empty((A.m, args.k), device=dev, dtype=torch.float64)
+        B = torch.rand((max(A.ncols, 1), args.k), generator=g, device=dev, dtype=tdt)
+        Cm = torch.empty((max(A.m, 1), args.k), device=dev, dtype=tdt)
         marker.fill_(1.0)                                   # boundary dispatch
         for _ in range(args.launches):
             mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), args.k, stream.cuda_stream)
         torch.cuda.synchronize()
         inf = mf.info()
         manifest.append({"gen": line, "m": int(A.m), "ncols": int(A.ncols), "nnz": int(A.nnz),
-                         "bytes_alg": S.bytes_alg(A.m, A.ncols, A.nnz, args.k, S.F64), "tiles": int(inf[19]),
-                         "split_rows": int(inf[6]), "windows": int(inf[12])})
-        del mf, B, Cm
+                         "bytes_alg": S.bytes_alg(A.m, A.ncols, A.nnz, args.k, S.F64 if args.dtype == "f64" else S.F32),
+                         "tiles": int(inf[19]), "split_rows": int(inf[6]), "windows": int(inf[12])})
+        mf.close()
+        del B, Cm, A
         print(f"{len(manifest)}/{len(lines)} {line}", flush=True)
     marker.fill_(1.0)
     torch.cuda.synchronize()
@@ -115,10 +132,12 @@ def per_matrix(disp, nmat):
 
 
 def collect(args):
-    outdir = ROOT / "gpurun_out" / "pmc_dataset"
+    import bench
+    outdir = ROOT / "gpurun_out" / "pmc_dataset" / args.tag
     outdir.mkdir(parents=True, exist_ok=True)
     manifest = outdir / "manifest.json"
-    drv = [sys.executable, str(Path(__file__).resolve()), "run", "--per-class", str(args.per_class), "--k", str(args.k),
+    drv = [sys.executable, str(Path(__file__).resolve()), "run", "--set", args.set, "--per-class", str(args.per_class),
+           "--stride", str(args.stride), "--offset", str(args.offset), "--k", str(args.k), "--dtype", args.dtype,
            "--launches", str(args.launches), "--max-nnz", str(args.max_nnz), "--manifest", str(manifest)]
     res = {}
     for i, extra in enumerate([["--kernel-trace"]] + [["--pmc", *p] for p in PASSES]):
@@ -132,36 +151,65 @@ def collect(args):
         man = json.loads(manifest.read_text())
         res[i] = per_matrix(dispatches(d), len(man))
         print(f"pass {i} {extra[-1]}: {len(man)} matrices ({time.time() - t0:.0f}s)", flush=True)
+    sha = bench.engine_sha256()
+    s = 8 if args.dtype == "f64" else 4
     with open(args.out, "w") as f:
         for j, mrec in enumerate(man):
             L = args.launches
             ms = res[0][j]["ns"] / L / 1e6
             rd = 2.0 * res[1][j]["FETCH_SIZE"] * 1024 / L
             wr = res[2][j]["WRITE_SIZE"] * 1024 / L
-            hit, miss = res[3][j].get("TCC_HIT_sum", 0.0), res[3][j].get("TCC_MISS_sum", 0.0)
-            rec = {**mrec, "k": args.k, "dtype": "f64", "kernel_ms": ms,
+            hit, miss = res[2][j].get("TCC_HIT_sum", 0.0) / L, res[2][j].get("TCC_MISS_sum", 0.0) / L
+            ach = bench.achievable(ms, rd + wr, hit + miss, float(mrec["ncols"]) * args.k * s)
+            rec = {**mrec, "k": args.k, "dtype": args.dtype, "engine_sha256": sha, "kernel_ms": ms,
                    "gflops": 2.0 * mrec["nnz"] * args.k / (ms * 1e-3) / 1e9,
                    "roofline_frac": mrec["bytes_alg"] / (ms * 1e-3) / 8e12,
                    "traffic_bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
                    "traffic_over_alg": (rd + wr) / mrec["bytes_alg"],
                    "traffic_tbs": (rd + wr) / (ms * 1e-3) / 1e12,
-                   "l2_hit": hit / max(hit + miss, 1.0)}
+                   "tcc_req": hit + miss, "l2_hit": hit / max(hit + miss, 1.0),
+                   "achievable_ms": ach["t_ms"] if ach else None,
+                   "frac_of_achievable": ach["frac_of_achievable"] if ach else None,
+                   "achievable_bound": ach["bound"] if ach else None}
             f.write(json.dumps(rec) + "\n")
     print(f"wrote {len(man)} records to {args.out}")
 
 
+def publish(args):
+    """Merge collected record files (--inputs) into profiles/pmc_dataset_latest.json, the file bench.py's dataset
+    sub-record reads (only records of the current engine build are kept)."""
+    import bench
+    sha = bench.engine_sha256()
+    recs = {}
+    for f in args.inputs:
+        for l in Path(f).read_text().splitlines():
+            if l.startswith("{"):
+                r = json.loads(l)
+                if r.get("engine_sha256") == sha:
+                    recs[(r["gen"], r["k"], r["dtype"])] = r
+    dest = ROOT / "profiles" / "pmc_dataset_latest.json"
+    dest.write_text(json.dumps({"engine_sha256": sha, "records": list(recs.values())}))
+    print(f"{dest}: {len(recs)} records of engine {sha[:12]}")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["run", "collect"])
+    ap.add_argument("mode", choices=["run", "collect", "publish"])
+    ap.add_argument("--inputs", nargs="*", default=[])
+    ap.add_argument("--set", choices=["stratified", "sample"], default="stratified")
     ap.add_argument("--per-class", type=int, default=6)
+    ap.add_argument("--stride", type=int, default=160)
+    ap.add_argument("--offset", type=int, default=0)
     ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--max-nnz", type=float, default=4.0e7)
     ap.add_argument("--timeout", type=int, default=500)
+    ap.add_argument("--tag", default="set")
     ap.add_argument("--manifest", default=str(ROOT / "gpurun_out" / "pmc_dataset" / "manifest.json"))
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "pmc_dataset" / "pmc_medium.jsonl"))
     args = ap.parse_args()
-    run(args) if args.mode == "run" else collect(args)
+    {"run": run, "collect": collect, "publish": publish}[args.mode](args)
 
 
 if __name__ == "__main__":

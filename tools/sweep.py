@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """tools/sweep.py -- dataset sweep driver (BASELINE configs 3/4: synthetic medium / large datasets, K sweep).
 
-For each generator line (from tools/medium_dataset.py, a file, or --line): generate the matrix once on the host,
-build one engine handle, and for every K: B = seeded U[0,1) resident in HBM (row-major), time `--iters` launches
-with HIP events on the launch stream (after `--warmup`), and check a sample of rows against the CPU oracle
-(bit-exact for rows <= the handle's split length T, normwise 1e-10 beyond).  One JSON line per (matrix, K) appended to --out; lines
-already present are skipped, so an interrupted sweep resumes where it stopped.  --budget bounds the wall time.
+For each generator line (spmm_amd.datasets, a file, or --line): generate the matrix once on the host (one line
+ahead, on a host thread), build one engine handle, and for every K: B = seeded U[0,1) resident in HBM (row-major),
+time `--iters` launches with HIP events on the launch stream (after `--warmup`), and check a sample of rows against
+the CPU oracle (bit-exact on the rows the engine reports exact, normwise 1e-10 on the rest).  One JSON line per
+(matrix, K) appended to --out, tagged with its dataset index and the engine build's fingerprint
+(bench.engine_sha256); lines already in --out, or whose index is in --done, are skipped, so a sweep resumes across
+gpurun calls (tools/sweep_resumable.sh).  --budget bounds the wall time.
 
   python tools/sweep.py --dataset medium --stride 60 --k 1,8,32,128 --out gpurun_out/sweep_medium.jsonl
 """
@@ -30,6 +32,26 @@ def twin_names() -> dict:
     """generator line -> name of the validation matrix it twins (reference config.sh:283-339)."""
     d = json.loads((ROOT / "spmm-research_amd" / "spmm_amd" / "validation_twins.json").read_text())["twins"]
     return {line: name for name, line in d.items()}
+
+
+def dataset_index_lines(args) -> list[tuple[int, str]]:
+    """(index in the full dataset / line list, line) for the selected stride and offset."""
+    if args.line:
+        return list(enumerate(args.line))
+    if args.dataset == "twins":
+        lines = list(json.loads((ROOT / "spmm-research_amd" / "spmm_amd" / "validation_twins.json").read_text())["twins"].values())
+    elif args.dataset == "medium":
+        from spmm_amd.datasets import medium_dataset_lines
+        lines = medium_dataset_lines()
+    else:
+        lines = [l.strip() for l in open(args.dataset) if l.strip()]
+    idx = list(range(len(lines)))
+    if getattr(args, "order", "dataset") == "interleave16":
+        bitrev4 = [int(f"{o:04b}"[::-1], 2) for o in range(16)]
+        idx.sort(key=lambda i: (bitrev4[i % 16], i))
+    if args.sort_by_size:
+        idx.sort(key=lambda i: int(lines[i].split()[0]) * float(lines[i].split()[2]))
+    return [(i, lines[i]) for i in idx[args.offset::args.stride]]
 
 
 def dataset_lines(args) -> list[str]:
@@ -110,6 +132,8 @@ def main():
     ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--offset", type=int, default=0)
     ap.add_argument("--sort-by-size", action="store_true")
+    ap.add_argument("--order", choices=["dataset", "interleave16"], default="dataset",
+                    help="interleave16: every 16th line first, then offsets 8, 4, 12, 2, ... (even class coverage)")
     ap.add_argument("--k", default="32")
     ap.add_argument("--dtype", default="f64", help="comma list of f64,f32")
     ap.add_argument("--warmup", type=int, default=3)
@@ -119,13 +143,18 @@ def main():
     ap.add_argument("--cpu-baseline", type=float, default=0.0,
                     help="seconds of reference-CPU timing per (matrix, K, dtype); 0 = none")
     ap.add_argument("--budget", type=float, default=1e9, help="seconds; stop starting new matrices after this")
+    ap.add_argument("--done", default=None, help="file of dataset line indices already swept (skipped)")
+    ap.add_argument("--no-features", action="store_true", help="skip the per-matrix feature extraction")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "sweep.jsonl"))
     args = ap.parse_args()
 
+    from concurrent.futures import ThreadPoolExecutor
     import torch
     import spmm_amd as S
     from oracle import oracle as O
+    import bench
 
+    sha = bench.engine_sha256()
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     dtypes = [d.strip() for d in args.dtype.split(",")]
@@ -142,22 +171,41 @@ def main():
                 done.add((d["gen"], d["k"], d["dtype"]))
             except Exception:
                 pass
+    done_idx = set()
+    if args.done and Path(args.done).exists():
+        done_idx = {int(x) for x in Path(args.done).read_text().split()}
     t_start = time.time()
     rng = np.random.default_rng(0)
-    for li, line in enumerate(dataset_lines(args)):
+    # (dataset index, line) still to do; matrices are generated one ahead on a host thread (the generator and the
+    # feature extractor release the GIL), so the GPU does not wait on the host between matrices
+    idx_lines = dataset_index_lines(args)
+    work = []
+    for idx, line in idx_lines:
+        if idx in done_idx:
+            continue
         todo = [(dt, k) for dt in dtypes for k in ks if (line, k, dt) not in done]
         if not todo:
             continue
-        if time.time() - t_start > args.budget:
-            print(f"budget reached after {li} lines", flush=True)
-            break
         p = S.gen_params(line)
         if p.nr_rows * p.avg_nnz_per_row > args.max_nnz:
             continue
+        work.append((idx, line, todo))
+
+    def prepare(line):
         t0 = time.time()
-        A = S.generate(p)
+        A = S.generate(S.gen_params(line))
         t_gen = time.time() - t0
-        feat = S.features(A)
+        feat = None if args.no_features else S.features(A)
+        return A, t_gen, feat
+
+    ex = ThreadPoolExecutor(max_workers=1)
+    fut = ex.submit(prepare, work[0][1]) if work else None
+    for wi, (idx, line, todo) in enumerate(work):
+        if time.time() - t_start > args.budget:
+            print(f"budget reached after {wi} lines", flush=True)
+            break
+        A, t_gen, feat = fut.result()
+        fut = ex.submit(prepare, work[wi + 1][1]) if wi + 1 < len(work) else None
         for dt in dtypes:
             dtype = np.float64 if dt == "f64" else np.float32
             tdtype = torch.float64 if dt == "f64" else torch.float32
@@ -169,8 +217,8 @@ def main():
                 mf.plan(k)
                 g = torch.Generator(device=dev)
                 g.manual_seed(42)
-                B = torch.rand((A.ncols, k), generator=g, device=dev, dtype=tdtype)
-                Cm = torch.empty((A.m, k), device=dev, dtype=tdtype)
+                B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
+                Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
                 run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
                 for _ in range(args.warmup):
                     run()
@@ -184,27 +232,31 @@ def main():
                 bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
                 par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows())
                 inf = mf.info()
-                rec = {"gen": line, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m), "nnz": int(A.nnz),
-                       "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9, "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9,
-                       "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12, "mem_mb": feat["mem_footprint"],
-                       "features": {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled", "skew",
-                                                         "avg_num_neighbours", "cross_row_similarity")},
-                       "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]), "panel_k": int(inf[10]),
-                       "split_rows": int(inf[6]), "blocks": int(inf[5]), "windows": int(inf[12]),
-                       "win_cols": int(inf[13]), "segments": int(inf[14]), "xcd": int(inf[15]), "lmax": int(inf[16]),
-                       "exact_rows": int(inf[17]), **par}
+                rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
+                       "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
+                       "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9, "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12,
+                       "engine_sha256": sha, "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
+                       "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
+                       "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
+                       "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
+                       **par}
+                if feat is not None:
+                    rec["mem_mb"] = feat["mem_footprint"]
+                    rec["features"] = {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled",
+                                                            "skew", "avg_num_neighbours", "cross_row_similarity")}
                 if args.cpu_baseline > 0:
                     x_col = np.ascontiguousarray(B.cpu().numpy().T).ravel()
                     rec.update(cpu_baseline(O, A, vals, x_col, k, args.cpu_baseline, cores))
                     rec["gpu_over_cpu"] = rec["gflops"] / rec["cpu_gflops"]
                 with open(out, "a") as f:
                     f.write(json.dumps(rec) + "\n")
-                print(json.dumps({k2: rec.get(k2) for k2 in ("name", "gen", "k", "dtype", "ms", "gflops",
+                print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
                                                              "roofline_frac", "cpu_gflops", "bitexact_seq_rows",
                                                              "normwise_ok")}), flush=True)
                 del B, Cm
             mf.close()
         del A
+    ex.shutdown(cancel_futures=True)
 
 
 if __name__ == "__main__":

@@ -1,14 +1,16 @@
 #!/bin/bash
-# Medium dataset at 1/16 (every 16th of the 16,190 parameter lines from --offset, ~1,012 matrices) x K in
-# {1,8,32,128}, resumable across gpurun calls: records already in profiles/<name>.part are skipped (the .part copy
-# travels with the tree; *.jsonl files do not), each call stops starting matrices after the budget (seconds).
-#   bash tools/sweep_resumable.sh <offset> <budget_s> <name>
+# Medium dataset (all 16,190 lines) x K in {1,8,32,128}, resumable across gpurun calls, one engine build:
+#   bash tools/sweep_resumable.sh <budget_s> <name> [k list]
+# Lines go in an interleaved order (every 16th line first, then the offsets 8, 4, 12, ...), so a partial sweep still
+# covers every class evenly.  profiles/<name>.done (dataset indices already swept; written by tools/sweep_merge.py
+# from the merged records -- small, it travels with the tree) is skipped; new records land in
+# gpurun_out/sweep/<name>.<stamp>.jsonl, and the call stops starting matrices after <budget_s>.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OFF=${1:-0}; BUDGET=${2:-1000}; NAME=${3:-r01_sweep_medium_s16_v8}
-OUT=gpurun_out/s16
+BUDGET=${1:-1000}; NAME=${2:-r03_sweep_medium}; KS=${3:-1,8,32,128}
+OUT=gpurun_out/sweep
 mkdir -p $OUT
-[ -f profiles/$NAME.part ] && cp profiles/$NAME.part $OUT/$NAME.jsonl
-timeout -k 10 1150 python -u tools/sweep.py --stride 16 --offset $OFF --k 1,8,32,128 --budget $BUDGET \
-    --out $OUT/$NAME.jsonl > $OUT/$NAME.log 2>&1
-rc=$?; tail -n 2 $OUT/$NAME.log | cut -c1-200; wc -l $OUT/$NAME.jsonl; exit $rc
+STAMP=$(date +%s)
+timeout -k 10 $((BUDGET + 170)) python -u tools/sweep.py --order interleave16 --k $KS --budget $BUDGET \
+    --done profiles/$NAME.done --out $OUT/$NAME.$STAMP.jsonl > $OUT/$NAME.$STAMP.log 2>&1
+rc=$?; tail -n 2 $OUT/$NAME.$STAMP.log | cut -c1-200; wc -l $OUT/$NAME.$STAMP.jsonl; exit $rc
