@@ -168,9 +168,12 @@ int root_source(spmm_hip_t *h, const void *d_b, int layout, int k, hipStream_t r
 int multi_plan(spmm_hip_t *h, int k) {
     MultiState &M = *h->multi;
     if (h->plan.k == k) return SPMM_HIP_OK;
-    for (spmm_hip_t *c : M.shard) {
+    for (size_t g = 0; g < M.shard.size(); ++g) {
+        spmm_hip_t *c = M.shard[g];
         int st = spmm_hip_plan(c, k);
         if (st != SPMM_HIP_OK) return st;
+        // every shard receives B and keeps its C rows in its own buffers; the root also stages host x
+        if ((st = ensure_buffers(c, true, g == 0, true))) return st;
     }
     Plan pl;
     pl.k = k;

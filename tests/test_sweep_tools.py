@@ -13,3 +13,32 @@ def test_medium_dataset_lines_match_published_set():
     for line in L[:50] + L[-50:]:
         f = line.split()
         assert len(f) == 11 and f[4] == "normal" and f[5] == "random" and f[10] == "14"
+
+
+def test_sample_parity_checks_exact_and_inexact_rows():
+    """tools/sweep.py's per-record check: exact rows bit for bit against the oracle, the others (only they need the
+    __float128 gold) normwise; a perturbed inexact row inside 1e-10 passes, one outside fails."""
+    import numpy as np
+    import torch
+    import spmm_amd as S
+    from oracle import oracle as O
+    import sweep
+    A = S.generate(S.gen_params("3000 3000 20 6.6667 normal random 0.3 100 0.95 0.5 14"))
+    k = 8
+    B = torch.from_numpy(O.drand48(5, A.ncols * k).reshape(A.ncols, k))
+    x_col = np.ascontiguousarray(B.numpy().T).ravel()
+    C = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, x_col, k)
+    exact = np.ones(A.m, bool)
+    exact[::7] = False
+    Ct = torch.from_numpy(C.copy())
+    r = sweep.sample_parity(S, O, A, B, Ct, k, 300, np.random.default_rng(0), np.float64, exact)
+    assert r["bitexact_seq_rows"] and r["normwise_ok"] and r["long_rows_checked"] > 0
+    Ct[::7] *= 1 + 1e-13                                # inexact rows, inside the bound
+    r = sweep.sample_parity(S, O, A, B, Ct, k, 3000, np.random.default_rng(0), np.float64, exact)
+    assert r["bitexact_seq_rows"] and r["normwise_ok"]
+    Ct[::7] *= 1 + 1e-8                                 # outside
+    r = sweep.sample_parity(S, O, A, B, Ct, k, 3000, np.random.default_rng(0), np.float64, exact)
+    assert r["bitexact_seq_rows"] and not r["normwise_ok"]
+    Ct[1] += 1e-300 if Ct[1, 0] == 0 else Ct[1, 0] * 1e-15   # an exact row one ulp-ish off
+    r = sweep.sample_parity(S, O, A, B, Ct, k, 3000, np.random.default_rng(0), np.float64, exact)
+    assert not r["bitexact_seq_rows"]
