@@ -153,15 +153,6 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
  * SPMM_HIP_TILES=-1 disables tiles, =1 takes every eligible tile; SPMM_HIP_TILE_REUSE=<x> sets the threshold. */
 int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out);
 
-/* Dense panel tiles of the current plan: runs of up to 64 consecutive rows whose union of columns
- * is dense (nnz / (rows x union) >= the policy density) are computed by spmm_panel_kernel, which stages per chunk of
- * 32 union columns the B rows and a zero-filled dense A panel in LDS; every tile row is still one left-to-right FMA
- * chain in CSR order (exact; a tile whose B holds a non-finite value is recomputed by the plain chain).  out has 6
- * slots: out[0]=tiles, out[1]=rows in tiles, out[2]=nonzeros in tiles, out[3]=chunks, out[4]=the sampled mean
- * density x 1000 the policy decided on, out[5]=1 when tiles run in XCD order.  SPMM_HIP_PANELS=-1 disables them,
- * =1 takes every run above SPMM_HIP_PANEL_DENSITY (default: the policy threshold). */
-int spmm_hip_panel_info(const spmm_hip_t *h, int64_t *out);
-
 /* Which C rows of the current plan are computed as ONE left-to-right FMA chain over the row in CSR order -- the
  * reference kernel's exact operation sequence, so bit-identical to it (mask[i] = 1); the others (rows longer than
  * the split length T, rows given vector lanes) are deterministic and within 1e-10 normwise.  mask has m bytes. */
@@ -254,23 +245,6 @@ int spmm_hip_debug_tiles(const int32_t *row_ptr, const int32_t *col_idx, int64_t
                          spmm_hip_tiles_t *out);
 void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t);
 
-/* Diagnostics (host only): the dense panel decomposition for a CSR pattern with sorted rows (tests).  Arrays
- * malloc'ed, release with spmm_hip_debug_panels_free:
- *   tiles[4*ntile]        {first row, rows, first chunk, chunks}
- *   chunks[4*(nchunk+1)]  {first tcol, columns (<= 32), first entry, entries} (+ sentinel)
- *   tcol[ncol]            union columns, chunk by chunk
- *   pos[nz], perm[nz]     entry -> (chunk-local column << 6) | tile-local row, and -> original nonzero
- *   in_tile[m]            1 for rows in a panel tile */
-typedef struct {
-    int64_t ntile, nchunk, ncol, nz, m;
-    int32_t *tiles, *chunks, *tcol;
-    uint16_t *pos;
-    int64_t *perm;
-    uint8_t *in_tile;
-} spmm_hip_panels_t;
-int spmm_hip_debug_panels(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
-                          double min_density, spmm_hip_panels_t *out);
-void spmm_hip_debug_panels_free(spmm_hip_panels_t *t);
 
 const char *spmm_hip_strerror(int status);
 const char *spmm_hip_last_error_detail(void);

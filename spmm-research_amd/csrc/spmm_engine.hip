@@ -107,8 +107,7 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 void free_plan(spmm_hip_t *h) {
     void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
                   h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr, h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg,
-                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm, h->d_ptiles, h->d_pchunk,
-                  h->d_pcol, h->d_pperm, h->d_rp, h->d_ppos, h->d_pval};
+                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
@@ -122,11 +121,6 @@ void free_plan(spmm_hip_t *h) {
     h->d_tstamps = nullptr;
     h->d_wperm = h->d_tperm = nullptr;
     h->nwperm = h->ntperm = 0;
-    h->d_ptiles = h->d_pchunk = nullptr;
-    h->d_pcol = h->d_pperm = h->d_rp = nullptr;
-    h->d_ppos = nullptr;
-    h->d_pval = nullptr;
-    h->npperm = 0;
     h->fuse = false;
     h->win_blk.clear();
     h->win_v.clear();
@@ -259,14 +253,13 @@ void launch_tiles_g(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t
             <<<h->plan.ntile, WG, 0, s>>>(h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg, (const T *)h->d_tval,
                                            h->d_tlidx, B, C, ld, h->d_tstamps);
     };
+    // S = 4 measured 1.3-2x slower everywhere and is not instantiated; S = 2 stays selectable
     using S1 = std::integral_constant<int, 1>;
     using S2 = std::integral_constant<int, (RPG % 2 == 0 && G >= 2) ? 2 : 1>;
-    using S4 = std::integral_constant<int, (RPG % 4 == 0 && G >= 4) ? 4 : 1>;
     auto go_x = [&](auto s_c) {
         if (h->plan.tile_xcd) go(std::true_type(), s_c); else go(std::false_type(), s_c);
     };
-    if (h->plan.tile_wide == 4) go_x(S4());
-    else if (h->plan.tile_wide == 2) go_x(S2());
+    if (h->plan.tile_wide == 2) go_x(S2());
     else go_x(S1());
 }
 
@@ -283,17 +276,6 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
     }
 }
 
-// Dense panel tiles for a panel of 256-byte B rows (checked at plan): P = 1 (16-byte piece per lane, 256 lanes).
-template <typename T>
-void launch_panels(spmm_hip_t *h, const T *B, T *C, int ld, hipStream_t s) {
-    auto go = [&](auto xcd_c) {
-        spmm_panel_kernel<T, 1, (bool)DEF_NTC, decltype(xcd_c)::value><<<h->plan.npanel, 256, 0, s>>>(
-            h->d_ptiles, h->d_pchunk, h->d_pcol, (const T *)h->d_pval, h->d_ppos, B, C, ld, h->d_rp, h->d_col,
-            (const T *)h->d_val);
-    };
-    if (h->plan.panel_xcd) go(std::true_type()); else go(std::false_type());
-}
-
 template <typename T>
 void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     T *P = (T *)h->d_part;
@@ -302,7 +284,6 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         const int kw = std::min(h->plan.kw, K - k0);
         if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
         if (h->plan.ntile > 0) launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
-        if (h->plan.npanel > 0) launch_panels<T>(h, B + k0, C + k0, K, s);
     }
     if (h->nlong > 0 && !h->fuse) {
         spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
@@ -919,135 +900,6 @@ double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64
     return n > 0 ? sum / (double)n : 0.0;
 }
 
-// ---------------------------------------------------------------------------------------------- dense panel tiles
-// PANEL mode (spmm_panel_kernel).  For rows whose union of columns is DENSE -- a run of 64 consecutive
-// rows inside a narrow band reads a large fraction of the band's B rows -- the work of a chunk of 32 union columns is
-// a small dense product C_tile[64][kw] += A_panel[64][32] * B_chunk[32][kw]: the kernel stages the chunk's B rows and
-// a zero-filled dense A panel in LDS (A travels sparse: value + 16-bit (column, row) position, scattered into the
-// panel), and every lane keeps 4 rows x one 16-byte piece of C in registers, reading per union column one B piece
-// and 4 panel values and doing 4 FMA groups -- no per-entry offsets, no per-row segments, a uniform loop.  A row's
-// chain visits the union columns in ascending order, which (rows sorted, no repeated column in a row) is its CSR
-// order, with fma(+0, b, acc) == acc exactly for a finite b in between: the rows stay bit-identical to the reference.
-// A tile whose staged B rows hold a non-finite value is recomputed from the CSR by the plain chain (the kernel checks).
-constexpr int PANEL_ROWS = PANEL_R;       // rows per panel tile (16 row quads x 4 rows per lane)
-constexpr int PANEL_UC = PANEL_U;         // union columns per chunk (8 KB of 256-B B rows, a 16 KB fp64 panel)
-constexpr int PANEL_COLMAX = PANEL_CMAX;  // union columns per tile (the kernel's LDS column list)
-constexpr int PANEL_DMAX = PANEL_D;       // chunk descriptors per tile (incl. the end marker)
-constexpr double PANEL_MIN_DENSITY = 0.15;   // policy: nnz / (rows x union) of a tile (§6.13)
-constexpr int64_t PANEL_MIN_TILES = 256;  // policy: candidate tiles (one workgroup each)
-constexpr uint16_t PANEL_POS_PAD = 0xFFFF;
-
-struct PanelPlan {
-    std::vector<int4> tiles;       // {first row, rows, first chunk, chunks}
-    std::vector<int4> chunks;      // {first tcol, columns, first entry, entries} + sentinel
-    std::vector<int32_t> tcol;     // union columns, chunk by chunk
-    std::vector<int64_t> perm;     // entry -> original nonzero
-    std::vector<uint16_t> pos;     // entry -> (chunk-local column << 6) | tile-local row
-    std::vector<uint8_t> in_tile;  // per row
-    int64_t rows = 0, nnz = 0;
-};
-
-// Rows a panel may take: at most T nonzeros and no column twice (a duplicate (row, col) pair would land on one
-// panel slot; the row kernel keeps such rows).
-bool panel_row_ok(const int32_t *rp, const int32_t *col, int64_t r, int T) {
-    if ((int64_t)rp[r + 1] - rp[r] > T) return false;
-    for (int64_t j = (int64_t)rp[r] + 1; j < rp[r + 1]; ++j)
-        if (col[j] == col[j - 1]) return false;
-    return true;
-}
-
-// Density of rows [r0, r1): nnz / (rows x distinct columns) (stamp/epoch marking), and the union size.
-double panel_density(const int32_t *rp, const int32_t *col, int64_t r0, int64_t r1, std::vector<int32_t> &stamp,
-                     int32_t epoch, int64_t *nu_out) {
-    int64_t nu = 0;
-    for (int64_t j = rp[r0]; j < rp[r1]; ++j)
-        if (stamp[(size_t)col[j]] != epoch) stamp[(size_t)col[j]] = epoch, ++nu;
-    if (nu_out) *nu_out = nu;
-    const int64_t nnz = (int64_t)rp[r1] - rp[r0];
-    return nu > 0 ? (double)nnz / ((double)(r1 - r0) * (double)nu) : 0.0;
-}
-
-// Build the panel tiles: runs of up to rmax consecutive eligible rows; a run is a tile when its density is >=
-// min_density and its union fits colmax columns and dmax - 1 chunks (else it is halved, down to 8 rows).
-bool build_panels(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int rmax, int uc,
-                  double min_density, int colmax, int dmax, PanelPlan &pp) {
-    pp = PanelPlan();
-    pp.in_tile.assign((size_t)m, 0);
-    std::vector<int32_t> stamp((size_t)ncols, -1), pos((size_t)ncols, 0), ulist;
-    int32_t epoch = 0;
-    auto next_epoch = [&]() {
-        if (epoch == INT32_MAX) std::fill(stamp.begin(), stamp.end(), -1), epoch = 0;
-        return ++epoch;
-    };
-    int64_t r = 0;
-    while (r < m) {
-        if (!panel_row_ok(rp, col, r, T)) {
-            ++r;
-            continue;
-        }
-        int64_t r1 = r;
-        while (r1 < m && r1 - r < rmax && panel_row_ok(rp, col, r1, T)) ++r1;
-        for (;;) {
-            int64_t nu = 0;
-            const double d = panel_density(rp, col, r, r1, stamp, next_epoch(), &nu);
-            const int64_t nch = (nu + uc - 1) / uc;
-            if (d >= min_density && nu > 0 && nu <= colmax && nch <= dmax - 1) {
-                ulist.clear();
-                const int32_t ep = next_epoch();
-                for (int64_t j = rp[r]; j < rp[r1]; ++j)
-                    if (stamp[(size_t)col[j]] != ep) stamp[(size_t)col[j]] = ep, ulist.push_back(col[j]);
-                std::sort(ulist.begin(), ulist.end());
-                for (size_t u = 0; u < ulist.size(); ++u) pos[(size_t)ulist[u]] = (int32_t)u;
-                const int c_first = (int)pp.chunks.size();
-                std::vector<int32_t> rowp(rp + r, rp + r1);
-                for (size_t u0 = 0; u0 < ulist.size(); u0 += (size_t)uc) {
-                    const size_t u1 = std::min(ulist.size(), u0 + (size_t)uc);
-                    const int64_t e0 = (int64_t)pp.perm.size();
-                    for (int64_t q = 0; q < r1 - r; ++q) {
-                        int32_t &p = rowp[(size_t)q];
-                        while (p < rp[r + q + 1] && (size_t)pos[(size_t)col[p]] < u1) {
-                            pp.perm.push_back(p);
-                            pp.pos.push_back((uint16_t)(((pos[(size_t)col[p]] - (int32_t)u0) << 6) | (int32_t)q));
-                            ++p;
-                        }
-                    }
-                    pp.chunks.push_back(make_int4((int)pp.tcol.size(), (int)(u1 - u0), (int)e0,
-                                                  (int)((int64_t)pp.perm.size() - e0)));
-                    pp.tcol.insert(pp.tcol.end(), ulist.begin() + (ptrdiff_t)u0, ulist.begin() + (ptrdiff_t)u1);
-                }
-                pp.tiles.push_back(make_int4((int)r, (int)(r1 - r), c_first, (int)pp.chunks.size() - c_first));
-                for (int64_t q = r; q < r1; ++q) pp.in_tile[(size_t)q] = 1;
-                pp.rows += r1 - r;
-                pp.nnz += (int64_t)rp[r1] - rp[r];
-                break;
-            }
-            if (d < min_density || r1 - r <= 8) break;        // too sparse (halving rarely densifies), or too small
-            r1 = r + (r1 - r) / 2;
-        }
-        r = r1;
-    }
-    pp.chunks.push_back(make_int4((int)pp.tcol.size(), 0, (int)pp.perm.size(), 0));
-    return !pp.tiles.empty();
-}
-
-// Policy gate: mean density over <= 256 evenly spaced candidate runs of rmax rows.
-double panel_density_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int rmax) {
-    if (m == 0) return 0.0;
-    std::vector<int32_t> stamp((size_t)ncols, -1);
-    const int64_t nt = (m + rmax - 1) / rmax, ns = std::min<int64_t>(256, nt);
-    double sum = 0.0;
-    int64_t n = 0;
-    for (int64_t i = 0; i < ns; ++i) {
-        const int64_t r0 = (i * nt / ns) * rmax, r1 = std::min<int64_t>(m, r0 + rmax);
-        bool ok = rp[r1] > rp[r0];
-        for (int64_t q = r0; q < r1 && ok; ++q) ok = panel_row_ok(rp, col, q, T);
-        if (!ok) continue;
-        sum += panel_density(rp, col, r0, r1, stamp, (int32_t)i, nullptr);
-        ++n;
-    }
-    return n > 0 ? sum / (double)n : 0.0;
-}
-
 }  // namespace
 
 extern "C" {
@@ -1253,47 +1105,12 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     }
 
     const int64_t srow_t = (int64_t)pl.kw * (int64_t)h->vsize;
-    // Dense panel tiles: runs of 64 rows whose union of columns is dense leave the row kernel for
-    // spmm_panel_kernel.  Needs 256-byte B rows per K panel (fp64 K=32 panels, fp32 K=64), sorted rows.
-    // SPMM_HIP_PANELS=-1 off / 1 every run with density >= SPMM_HIP_PANEL_DENSITY (default: the policy threshold,
-    // also with fewer tiles than the policy's minimum).
-    PanelPlan pp;
-    bool panels = false;
-    {
-        const int forced = env_int("SPMM_HIP_PANELS", 0);
-        const char *thr = getenv("SPMM_HIP_PANEL_DENSITY");
-        const double min_d = (thr && *thr) ? atof(thr) : PANEL_MIN_DENSITY;
-        const bool shape_ok = h->nnz > 0 && srow_t == 256 && k % pl.kw == 0 && ((int64_t)k * h->vsize) % 16 == 0 &&
-                              h->m > 0 && h->ncols < INT32_MAX;
-        const int64_t win_forced = h->var.win_bytes != 0 ? h->var.win_bytes : (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
-        const int tiles_forced = h->var.tiles != 0 ? h->var.tiles : env_int("SPMM_HIP_TILES", 0);
-        if (forced >= 0 && shape_ok && win_forced <= 0 && tiles_forced <= 0) {
-            if (int st = load_cols()) return st;
-            if (rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
-                pl.panel_density = panel_density_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max,
-                                                        PANEL_ROWS);
-                const bool enough = (h->m + PANEL_ROWS - 1) / PANEL_ROWS >= PANEL_MIN_TILES;
-                if (forced > 0 || (enough && pl.panel_density >= min_d))
-                    panels = build_panels(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, PANEL_ROWS,
-                                          PANEL_UC, min_d, PANEL_COLMAX - 4, PANEL_DMAX, pp);
-                if (panels && forced <= 0 && (int64_t)pp.tiles.size() < PANEL_MIN_TILES / 4) panels = false;
-                if (panels && (int64_t)pp.perm.size() + PAD_BYTES >= tile_index_limit()) panels = false;
-            }
-        }
-        if (panels) {
-            pl.npanel = (int)pp.tiles.size();
-            pl.panel_rows = pp.rows;
-            pl.panel_nnz = pp.nnz;
-            pl.panel_chunks = (int64_t)pp.chunks.size() - 1;
-            pl.panel_xcd = (env_int("SPMM_HIP_TILE_XCD", 1) > 0 && pl.npanel >= 64) ? 1 : 0;
-        }
-    }
     // LDS B tiles: rows whose union of columns is reused enough leave the row kernel.  Needs 16-byte
     // B pieces in every panel and sorted rows.  SPMM_HIP_TILES=-1 off / 1 every eligible tile; SPMM_HIP_TILE_REUSE
     // sets the policy threshold.
     TilePlan tp;
     bool tiles = false;
-    if (!panels) {
+    {
         const int64_t srow = srow_t;
         const int env_t = env_int("SPMM_HIP_TILES", 0);
         const int forced = h->var.tiles != 0 ? h->var.tiles : env_t;
@@ -1331,7 +1148,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             pl.tile_xcd = (env_x > 0 && pl.ntile >= 64) ? 1 : 0;
             // compute-lane width in 16-byte pieces: the requested 1/2/4, lowered until rows per group divide
             int sw = std::max(1, env_int("SPMM_HIP_TILE_WIDE", TILE_WIDE_DEFAULT));
-            sw = sw >= 4 ? 4 : sw >= 2 ? 2 : 1;
+            sw = sw >= 2 ? 2 : 1;
             while (sw > 1 && tile_rpg(g_t) % sw != 0) sw /= 2;
             pl.tile_wide = sw;
         }
@@ -1352,7 +1169,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             if (int st = load_cols()) return st;
         }
         pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
-        if (!tiles && !panels && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) &&
+        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) &&
             rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
             std::vector<Piece> pcs;
             Inspection tmp;
@@ -1368,7 +1185,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         pl.nseg = (int64_t)in.vdest.size();
     } else {
         inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd,
-                tiles ? tp.in_tile.data() : panels ? pp.in_tile.data() : nullptr, pl.block_rows);
+                tiles ? tp.in_tile.data() : nullptr, pl.block_rows);
         pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
     }
     h->nv = (int64_t)in.vrow_ptr.size() - 1;
@@ -1384,7 +1201,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         const int lcap = std::max(1, 64 / g);
         // the rows the row kernel runs: gap virtual rows and the tile rows' nonzeros are not among them
         const double nvr = (double)((int64_t)in.vrow_ptr.size() - 1 - in.ngaps);
-        const double nnz_rows = (double)(h->nnz - (tiles ? tp.nnz : 0) - (panels ? pp.nnz : 0));
+        const double nnz_rows = (double)(h->nnz - (tiles ? tp.nnz : 0));
         const double rows_per_block = in.blk.empty() ? 0.0 : nvr / (double)in.blk.size();
         const double mean_vrow = nvr > 0 ? nnz_rows / nvr : 0.0;
         const int env_l = env_int("SPMM_HIP_LANES", 0);
@@ -1547,27 +1364,6 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         h->insp_bytes += tp.tiles.size() * sizeof(int4) + tp.chunks.size() * sizeof(int4) + tp.tcol.size() * 4 +
                          tp.tseg.size() * 2 + tp.tlidx.size() * 2 + tval.size();
     }
-    if (e == hipSuccess && panels) {
-        // entries chunk-major: values (re-gathered on value updates through d_pperm), positions, union columns
-        std::vector<char> hval((size_t)h->nnz * h->vsize);
-        e = hipMemcpy(hval.data(), h->d_val, hval.size(), hipMemcpyDeviceToHost);
-        const size_t nz = pp.perm.size();
-        std::vector<char> pval(nz * h->vsize + PAD_BYTES, 0);
-        for (size_t q = 0; q < nz; ++q) std::memcpy(&pval[q * h->vsize], &hval[(size_t)pp.perm[q] * h->vsize], h->vsize);
-        pp.pos.resize(nz + PAD_BYTES / 2, PANEL_POS_PAD);
-        pp.tcol.resize(pp.tcol.size() + PAD_BYTES / 4, 0);
-        std::vector<int32_t> pperm(pp.perm.begin(), pp.perm.end());
-        h->npperm = (int64_t)pperm.size();
-        if (e == hipSuccess) e = alloc_copy((void **)&h->d_ptiles, pp.tiles.data(), pp.tiles.size() * sizeof(int4));
-        if (e == hipSuccess) e = alloc_copy((void **)&h->d_pchunk, pp.chunks.data(), pp.chunks.size() * sizeof(int4));
-        if (e == hipSuccess) e = alloc_copy((void **)&h->d_pcol, pp.tcol.data(), pp.tcol.size() * 4);
-        if (e == hipSuccess) e = alloc_copy((void **)&h->d_ppos, pp.pos.data(), pp.pos.size() * 2);
-        if (e == hipSuccess) e = alloc_copy(&h->d_pval, pval.data(), pval.size());
-        if (e == hipSuccess) e = alloc_copy((void **)&h->d_pperm, pperm.data(), pperm.size() * 4);
-        if (e == hipSuccess) e = alloc_copy((void **)&h->d_rp, h->h_row_ptr.data(), h->h_row_ptr.size() * 4);
-        h->insp_bytes += pp.tiles.size() * sizeof(int4) + pp.chunks.size() * sizeof(int4) + pp.tcol.size() * 4 +
-                         pp.pos.size() * 2 + pval.size() + pperm.size() * 4 + h->h_row_ptr.size() * 4;
-    }
     if (e != hipSuccess) {
         free_plan(h);
         return fail(e == hipErrorOutOfMemory ? SPMM_HIP_ERR_NOMEM : SPMM_HIP_ERR_HIP,
@@ -1719,7 +1515,6 @@ int update_values(spmm_hip_t *h, const void *vals, hipMemcpyKind kind, hipStream
     };
     if (int st = gather(h->d_wperm, h->d_wval, h->nwperm)) return st;
     if (int st = gather(h->d_tperm, h->d_tval, h->ntperm)) return st;
-    if (int st = gather(h->d_pperm, h->d_pval, h->npperm)) return st;
     return SPMM_HIP_OK;
 }
 }  // namespace
@@ -1915,17 +1710,6 @@ int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out) {
     return SPMM_HIP_OK;
 }
 
-int spmm_hip_panel_info(const spmm_hip_t *h, int64_t *out) {
-    if (!h || !out) return fail(SPMM_HIP_ERR_ARG, "panel_info: bad arguments");
-    out[0] = h->plan.npanel;
-    out[1] = h->plan.panel_rows;
-    out[2] = h->plan.panel_nnz;
-    out[3] = h->plan.panel_chunks;
-    out[4] = (int64_t)(h->plan.panel_density * 1000.0 + 0.5);
-    out[5] = h->plan.panel_xcd;
-    return SPMM_HIP_OK;
-}
-
 int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask) {
     if (!h || !mask || h->plan.k < 1) return fail(SPMM_HIP_ERR_ARG, "exact_rows: handle not planned");
     if (h->m > 0) std::memcpy(mask, h->exact.data(), (size_t)h->m);
@@ -2024,45 +1808,6 @@ int spmm_hip_debug_tiles(const int32_t *row_ptr, const int32_t *col_idx, int64_t
     out->perm = dup(tp.perm);
     out->in_tile = dup(tp.in_tile);
     return SPMM_HIP_OK;
-}
-
-int spmm_hip_debug_panels(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t T,
-                          double min_density, spmm_hip_panels_t *out) {
-    if (!row_ptr || !out || m < 0 || ncols < 0 || T < 1 || (!col_idx && m > 0 && row_ptr[m] > 0))
-        return fail(SPMM_HIP_ERR_ARG, "debug_panels: bad arguments");
-    std::memset(out, 0, sizeof(*out));
-    if (!rows_sorted(row_ptr, col_idx, m)) return fail(SPMM_HIP_ERR_CSR, "debug_panels: unsorted row");
-    PanelPlan pp;
-    build_panels(row_ptr, col_idx, m, ncols, T, PANEL_ROWS, PANEL_UC, min_density, PANEL_COLMAX - 4, PANEL_DMAX, pp);
-    auto dup = [](const auto &v) {
-        using E = typename std::decay_t<decltype(v)>::value_type;
-        E *p = (E *)malloc(std::max<size_t>(v.size(), 1) * sizeof(E));
-        if (p && !v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(E));
-        return p;
-    };
-    out->ntile = (int64_t)pp.tiles.size();
-    out->nchunk = (int64_t)pp.chunks.size() - 1;
-    out->ncol = (int64_t)pp.tcol.size();
-    out->nz = (int64_t)pp.perm.size();
-    out->m = m;
-    out->tiles = (int32_t *)dup(pp.tiles);
-    out->chunks = (int32_t *)dup(pp.chunks);
-    out->tcol = dup(pp.tcol);
-    out->pos = dup(pp.pos);
-    out->perm = dup(pp.perm);
-    out->in_tile = dup(pp.in_tile);
-    return SPMM_HIP_OK;
-}
-
-void spmm_hip_debug_panels_free(spmm_hip_panels_t *t) {
-    if (!t) return;
-    free(t->tiles);
-    free(t->chunks);
-    free(t->tcol);
-    free(t->pos);
-    free(t->perm);
-    free(t->in_tile);
-    std::memset(t, 0, sizeof(*t));
 }
 
 void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t) {

@@ -47,10 +47,6 @@ struct Plan {
     int tile_wide = 1;         // compute-lane width in 16-byte pieces of a B row (1, 2, 4), where RPG allows
     int64_t tile_rows = 0, tile_nnz = 0, tile_chunks = 0;
     double tile_reuse = 0.0;   // sampled mean reuse (nnz per union column) the policy saw
-    int npanel = 0;            // dense panel tiles (spmm_panel_kernel), rows and nonzeros they cover, their chunks
-    int panel_xcd = 0;
-    int64_t panel_rows = 0, panel_nnz = 0, panel_chunks = 0;
-    double panel_density = 0.0;   // sampled mean density (nnz / rows x union) the policy saw
 };
 
 struct Variant {
@@ -113,11 +109,6 @@ struct spmm_hip_handle {
     long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
     int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)
     int32_t *d_tperm = nullptr;      // tile chunk-major position -> nonzero, -1 = padding (value updates re-gather tval)
-    int4 *d_ptiles = nullptr, *d_pchunk = nullptr;  // panel mode (spmm_panel_kernel)
-    int32_t *d_pcol = nullptr, *d_pperm = nullptr, *d_rp = nullptr;   // union columns, entry -> nonzero, row_ptr
-    uint16_t *d_ppos = nullptr;
-    void *d_pval = nullptr;
-    int64_t npperm = 0;
     int64_t nwperm = 0, ntperm = 0;
 
     // per-k buffers

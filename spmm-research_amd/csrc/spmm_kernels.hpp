@@ -672,171 +672,6 @@ __global__ __launch_bounds__(WG, TILE_WGS) void spmm_tile_kernel(const int4 *__r
     }
 }
 
-// ------------------------------------------------------------------------------------------------ dense panels
-// PANEL mode (inspector build_panels in spmm_engine.hip).  A panel tile is up to 64 consecutive C rows
-// whose union of columns is dense; its union is cut into chunks of <= 32 columns.  Per chunk the workgroup stages in
-// LDS (a) the chunk's B rows (256 bytes each: 16 pieces of 16 B) and (b) a zero-filled dense A panel [32][64] into
-// which the chunk's entries (value, (column << 6) | row) are scattered.  Lane (row quad rq, piece group cg) owns rows
-// 4rq .. 4rq+3 and P consecutive 16-byte pieces of the C row; per union column u it reads P B pieces and the 4 panel
-// values of its rows and does 4 x P vector FMAs.  Every row's chain runs over the union columns in ascending order:
-// its own nonzeros in CSR order (rows sorted, no column twice) with fma(+0, b, acc) == acc in between, exact for a
-// finite b (acc starts at +0 and can never become -0).  Lanes check every staged B value; a tile that staged a
-// non-finite one is recomputed row by row from the CSR (the reference's chain, so inf/NaN propagate as there).
-//   ptiles[t]  = {first C row, rows, first chunk, chunks};  pchunk[c] = {first tcol, columns, first entry, entries}
-constexpr int PANEL_R = 64;                   // rows per panel tile
-constexpr int PANEL_U = 32;                   // union columns per chunk
-constexpr int PANEL_CMAX = 3072;              // union columns per tile (LDS list)
-constexpr int PANEL_D = 128;                  // chunk descriptors per tile (incl. the end marker)
-
-template <typename T, int P, bool NTC, bool XCD>
-__global__ __launch_bounds__(256 / P, 4) void spmm_panel_kernel(const int4 *__restrict__ ptiles,
-                                                               const int4 *__restrict__ pchunk,
-                                                               const int32_t *__restrict__ pcol,
-                                                               const T *__restrict__ pval,
-                                                               const uint16_t *__restrict__ ppos,
-                                                               const T *__restrict__ B, T *__restrict__ C, int ld,
-                                                               const int32_t *__restrict__ row_ptr,
-                                                               const int32_t *__restrict__ col_idx,
-                                                               const T *__restrict__ vals) {
-    constexpr int NT = 256 / P;                    // lanes: 16 row quads x 16/P piece groups
-    constexpr int VEC = 16 / (int)sizeof(T);       // values per 16-byte piece
-    constexpr int CPQ = 16 / P;                    // piece groups per row quad
-    constexpr int NBP = PANEL_U * 16 / NT;         // staged B pieces per lane per chunk
-    constexpr int EPL = PANEL_U * PANEL_R / NT;    // panel entries per lane per chunk (at most)
-    constexpr int NZ = PANEL_U * PANEL_R * (int)sizeof(T) / 16 / NT;   // 16-byte zero stores per lane
-    using V = vec<T, VEC>;
-    __shared__ __attribute__((aligned(16))) V sB[PANEL_U * 16];
-    __shared__ __attribute__((aligned(16))) T sA[PANEL_U * PANEL_R];
-    __shared__ __attribute__((aligned(16))) int4 sdesc[PANEL_D];
-    __shared__ __attribute__((aligned(16))) int32_t scol[PANEL_CMAX];
-    __shared__ int sbad;
-
-    const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-    const int4 tl = ptiles[b];
-    const int tid = threadIdx.x, wave = tid / 64, wl = tid % 64;
-    const int rq = tid / CPQ, cg = tid % CPQ;
-    if (tid == 0) sbad = 0;
-    // prologue: the tile's chunk descriptors and union columns into LDS (one LDS-DMA round trip)
-    {
-        typedef __attribute__((address_space(3))) void lds_void;
-        const int col0 = pchunk[tl.z].x, col1 = pchunk[tl.z + tl.w].x, c0a = col0 & ~3;
-        const int nd = (tl.w + 1) * 16, ncb = ((col1 - c0a + 3) & ~3) * 4;
-        for (int q = wave; q * 1024 < nd; q += NT / 64) {
-            const int off = q * 1024 + wl * 16;
-            if (off < nd)
-                __builtin_amdgcn_global_load_lds((const void *)((const char *)(pchunk + tl.z) + off),
-                                                 (lds_void *)((char *)sdesc + q * 1024), 16, 0, 0);
-        }
-        for (int q = wave; q * 1024 < ncb; q += NT / 64) {
-            const int off = q * 1024 + wl * 16;
-            if (off < ncb)
-                __builtin_amdgcn_global_load_lds((const void *)((const char *)(pcol + c0a) + off),
-                                                 (lds_void *)((char *)scol + q * 1024), 16, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    const int cbase = pchunk[tl.z].x & ~3;
-
-    V acc[4][P];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int p = 0; p < P; ++p) acc[q][p] = vzero<T, VEC>();
-    const char *Bb = reinterpret_cast<const char *>(B);
-    const size_t ldb = (size_t)ld * sizeof(T);
-    // chunk staging registers: loads are unconditional (indices clamped into the chunk) and only the LDS writes are
-    // predicated, so no partly defined register makes the compiler drain the load queue early
-    i32x4 rb[NBP];
-    T rv[EPL];
-    uint16_t rp_[EPL];
-    int nb = 0, ne = 0;
-    auto load = [&](int c) {
-        const int4 ch = sdesc[c];
-        nb = ch.y * 16;
-        ne = ch.w;
-#pragma unroll
-        for (int it = 0; it < NBP; ++it) {
-            const int p = min(it * NT + tid, nb - 1);
-            const int row = scol[ch.x - cbase + (p >> 4)];
-            rb[it] = *reinterpret_cast<const i32x4 *>(Bb + (size_t)row * ldb + (p & 15) * 16);
-        }
-#pragma unroll
-        for (int it = 0; it < EPL; ++it) {
-            const int e = ch.z + max(0, min(it * NT + tid, ne - 1));
-            rv[it] = __builtin_nontemporal_load(pval + e);
-            rp_[it] = __builtin_nontemporal_load(ppos + e);
-        }
-    };
-    bool bad = false;
-    load(0);
-    for (int c = 0; c < tl.w; ++c) {
-        const int ncol = sdesc[c].y;
-        __syncthreads();                                    // chunk c-1 consumed by every wave
-#pragma unroll
-        for (int it = 0; it < NZ; ++it)
-            reinterpret_cast<i32x4 *>(sA)[it * NT + tid] = i32x4{0, 0, 0, 0};
-#pragma unroll
-        for (int it = 0; it < NBP; ++it)
-            if (it * NT + tid < nb) {
-                reinterpret_cast<i32x4 *>(sB)[it * NT + tid] = rb[it];
-                V v;
-                __builtin_memcpy(&v, &rb[it], 16);
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) bad |= !__builtin_isfinite(v.v[i]);
-            }
-        __syncthreads();                                    // panel zeroed
-#pragma unroll
-        for (int it = 0; it < EPL; ++it)
-            if (it * NT + tid < ne) sA[(rp_[it] >> 6) * PANEL_R + (rp_[it] & 63)] = rv[it];
-        __syncthreads();                                    // chunk c staged
-        load(min(c + 1, tl.w - 1));                         // chunk c+1 in flight during the compute
-        // register ping-pong: column u+1's panel values and B pieces are in flight while column u's FMAs issue (the
-        // read one past the chunk's last column stays inside the LDS allocation and is never used)
-        const T *arow = sA + rq * 4;
-        const V *brow = sB + cg * P;
-        vec<T, 4> a = *reinterpret_cast<const vec<T, 4> *>(arow);
-        V bv[P];
-#pragma unroll
-        for (int p = 0; p < P; ++p) bv[p] = brow[p];
-#pragma unroll 2
-        for (int u = 0; u < ncol; ++u) {
-            const vec<T, 4> an = *reinterpret_cast<const vec<T, 4> *>(arow + (u + 1) * PANEL_R);
-            V bn[P];
-#pragma unroll
-            for (int p = 0; p < P; ++p) bn[p] = brow[(u + 1) * 16 + p];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int p = 0; p < P; ++p) vfma(acc[q][p], a.v[q], bv[p]);
-            a = an;
-#pragma unroll
-            for (int p = 0; p < P; ++p) bv[p] = bn[p];
-        }
-    }
-    if (bad) sbad = 1;                                      // a benign race: every writer stores 1
-    __syncthreads();
-    if (sbad) {
-        // non-finite B in this tile: each row is one plain left-to-right chain over its CSR nonzeros (the reference's
-        // operation sequence; inf / NaN propagate exactly where the reference's do)
-        for (int rr = tid / 16; rr < tl.y; rr += NT / 16) {
-            const int row = tl.x + rr, pc = tid % 16;
-            V a = vzero<T, VEC>();
-            for (int j = row_ptr[row]; j < row_ptr[row + 1]; ++j)
-                vfma(a, vals[j], *reinterpret_cast<const V *>(B + (size_t)col_idx[j] * ld + pc * VEC));
-            vstore<T, VEC, NTC>(C + (size_t)row * ld + pc * VEC, a);
-        }
-        return;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int r = rq * 4 + q;
-        if (r < tl.y)
-#pragma unroll
-            for (int p = 0; p < P; ++p) vstore<T, VEC, NTC>(C + (size_t)(tl.x + r) * ld + (cg * P + p) * VEC, acc[q][p]);
-    }
-}
-
 // long_rows[b] = {row, first_slot, nslots, 0}: C[row][n] = sum of the row's partial slots P[first_slot + q][n].
 // Separate combine launch (column-window plans, or partials beyond 4 GiB): one workgroup per split row.
 template <typename T>

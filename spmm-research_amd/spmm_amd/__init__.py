@@ -100,12 +100,6 @@ class _Tiles(C.Structure):
                 ("in_tile", C.POINTER(C.c_uint8))]
 
 
-class _Panels(C.Structure):
-    _fields_ = [("ntile", _i64), ("nchunk", _i64), ("ncol", _i64), ("nz", _i64), ("m", _i64),
-                ("tiles", C.POINTER(C.c_int32)), ("chunks", C.POINTER(C.c_int32)), ("tcol", C.POINTER(C.c_int32)),
-                ("pos", C.POINTER(C.c_uint16)), ("perm", C.POINTER(C.c_int64)), ("in_tile", C.POINTER(C.c_uint8))]
-
-
 def _bind_hip(L: C.CDLL) -> C.CDLL:
     vp, i32, i64 = C.c_void_p, C.c_int32, _i64
     L.spmm_hip_create.argtypes = [_i32p, _i32p, vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)]
@@ -134,10 +128,6 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_debug_free.argtypes = [C.POINTER(_Inspection)]
     L.spmm_hip_debug_free.restype = None
     L.spmm_hip_tile_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
-    L.spmm_hip_panel_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
-    L.spmm_hip_debug_panels.argtypes = [_i32p, _i32p, i64, i64, i32, C.c_double, C.POINTER(_Panels)]
-    L.spmm_hip_debug_panels_free.argtypes = [C.POINTER(_Panels)]
-    L.spmm_hip_debug_panels_free.restype = None
     L.spmm_hip_run_rowmajor.argtypes = [vp, vp, vp, i32]
     L.spmm_hip_update_values.argtypes = [vp, vp]
     L.spmm_hip_update_values_device.argtypes = [vp, vp, vp]
@@ -377,24 +367,6 @@ def debug_tiles(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, T: int, rm
     return out
 
 
-def debug_panels(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, T: int = 2048, min_density: float = 0.15) -> dict:
-    """The dense panel decomposition (host only; spmm_hip_debug_panels): tiles, chunks, union columns, entry
-    positions ((chunk-local column << 6) | tile-local row), entry -> nonzero, rows in tiles."""
-    rp = np.ascontiguousarray(row_ptr, np.int32)
-    ci = np.ascontiguousarray(col_idx if len(col_idx) else np.zeros(1), np.int32)
-    t = _Panels()
-    _check("debug_panels", hip.spmm_hip_debug_panels(rp, ci, len(rp) - 1, ncols, T, min_density, C.byref(t)))
-    try:
-        def arr(p, n):
-            return np.ctypeslib.as_array(p, (max(n, 1),))[:n].copy()
-        out = {"tiles": arr(t.tiles, 4 * t.ntile).reshape(-1, 4), "chunks": arr(t.chunks, 4 * (t.nchunk + 1)).reshape(-1, 4),
-               "tcol": arr(t.tcol, t.ncol), "pos": arr(t.pos, t.nz), "perm": arr(t.perm, t.nz),
-               "in_tile": arr(t.in_tile, t.m).astype(bool)}
-    finally:
-        hip.spmm_hip_debug_panels_free(C.byref(t))
-    return out
-
-
 def device_count() -> int:
     n = C.c_int()
     hip.spmm_hip_device_count(C.byref(n))
@@ -509,13 +481,6 @@ class MatrixFormat:
         _check("tile_info", hip.spmm_hip_tile_info(self._h, out))
         return {"tiles": int(out[0]), "rows": int(out[1]), "nnz": int(out[2]), "chunks": int(out[3]),
                 "reuse": out[4] / 1000.0, "xcd": int(out[5]), "wide": int(out[6])}
-
-    def panel_info(self) -> dict:
-        """Dense panel tiles of the current plan (spmm_hip_panel_info)."""
-        out = np.zeros(6, np.int64)
-        _check("panel_info", hip.spmm_hip_panel_info(self._h, out))
-        return {"tiles": int(out[0]), "rows": int(out[1]), "nnz": int(out[2]), "chunks": int(out[3]),
-                "density": out[4] / 1000.0, "xcd": int(out[5])}
 
     def exact_rows(self) -> np.ndarray:
         """bool[m]: rows computed as the reference's single left-to-right FMA chain (bit-identical to it)."""

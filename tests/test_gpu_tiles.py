@@ -185,7 +185,8 @@ def test_tile_policy_gates(env, monkeypatch):
 def test_tiles_wide_lanes_bitexact(env, monkeypatch, line, k, dtype, sw):
     """Wide compute lanes (SPMM_HIP_TILE_WIDE=S: S 16-byte pieces of a B row per lane, 1/S the lanes per row, same
     tile geometry) compute the same FMA chains: bit-identical to 16-byte lanes and to the oracle.  The width drops
-    to what the rows per group allow (B rows >= 128 B for S=2, >= 256 B for S=4)."""
+    to what the rows per group allow (B rows >= 128 B for S=2); S=4 (measured slower) is no longer built: asking
+    for it gives S=2."""
     torch, S, O = env
     A = S.generate(S.gen_params(line))
     x = O.drand48(11 + k, A.ncols * k)
@@ -195,7 +196,7 @@ def test_tiles_wide_lanes_bitexact(env, monkeypatch, line, k, dtype, sw):
     y0, t0, ex0, _ = run(S, A, vals, xx, k, 1, monkeypatch, {"SPMM_HIP_TILE_WIDE": "1"})
     assert t1["tiles"] > 0 and t0["tiles"] == t1["tiles"] and t0["wide"] == 1
     rb = k * vals.itemsize
-    assert t1["wide"] == (sw if rb >= 64 * sw else 2 if rb >= 128 else 1)
+    assert t1["wide"] == (2 if rb >= 128 else 1)
     assert np.array_equal(ex0, ex1)
     assert np.array_equal(bits(y1), bits(y0))
     check(O, A, vals, xx, k, y1, ex1)
