@@ -38,6 +38,11 @@ PASSES = [["FETCH_SIZE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]]
 
 
 def lines_for(args):
+    i, n = (int(x) for x in getattr(args, "part", "0/1").split("/"))
+    return _lines_for(args)[i::n]
+
+
+def _lines_for(args):
     from spmm_amd.datasets import medium_dataset_lines
     L = medium_dataset_lines()
     if args.set == "sample":
@@ -136,7 +141,8 @@ def collect(args):
     outdir = ROOT / "gpurun_out" / "pmc_dataset" / args.tag
     outdir.mkdir(parents=True, exist_ok=True)
     manifest = outdir / "manifest.json"
-    drv = [sys.executable, str(Path(__file__).resolve()), "run", "--set", args.set, "--per-class", str(args.per_class),
+    drv = [sys.executable, str(Path(__file__).resolve()), "run", "--set", args.set, "--part", args.part,
+           "--per-class", str(args.per_class),
            "--stride", str(args.stride), "--offset", str(args.offset), "--k", str(args.k), "--dtype", args.dtype,
            "--launches", str(args.launches), "--max-nnz", str(args.max_nnz), "--manifest", str(manifest)]
     res = {}
@@ -198,6 +204,7 @@ def main():
     ap.add_argument("--inputs", nargs="*", default=[])
     ap.add_argument("--set", choices=["stratified", "sample"], default="stratified")
     ap.add_argument("--per-class", type=int, default=6)
+    ap.add_argument("--part", default="0/1", help="i/n: every n-th line of the set from i (split a set over calls)")
     ap.add_argument("--stride", type=int, default=160)
     ap.add_argument("--offset", type=int, default=0)
     ap.add_argument("--k", type=int, default=32)
