@@ -106,7 +106,8 @@ def parse():
     ap.add_argument("--twins-cpu-seconds", type=float, default=1.0, help="twins: CPU-baseline budget per twin/dtype")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-warmup", type=int, default=100, help="CPU-baseline warm-up calls (reference harness: 100)")
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget of timed CPU-baseline calls")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="budget of timed CPU-baseline calls (the reference's 100 timed calls fit ~9 s on 16 cores)")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"),
                     help="config-2 per-launch PMC counters (tools/collect_pmc.py)")
     ap.add_argument("--pmc-dataset", default=str(ROOT / "profiles" / "pmc_dataset_latest.json"),
@@ -228,11 +229,22 @@ def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
     times.sort()
     t = times[len(times) // 2]
     gf = 2.0 * A.nnz * k / t / 1e9
+    # the reference harness's own B (x = 1.0, spmv_bench.cpp:901) as well: BASELINE.md asks for both
+    ones = np.ones_like(x)
+    fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, ones, y, k, threads)
+    t1 = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, ones, y, k, threads)
+        t1.append(time.perf_counter() - t0)
+    t_ones = sorted(t1)[2]
     return {"value": round(gf, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+            "value_x_ones": round(2.0 * A.nnz * k / t_ones / 1e9, 3),
             "sample": (f"full matrix, same A and x (drand48 seed 42, column-major) as the GPU run; oracle/liboracle.so "
                        f"(C restatement of compute_csr, bit-identical to the reference build); {threads} OpenMP threads "
                        f"(OMP_PROC_BIND=true OMP_PLACES=cores OMP_DYNAMIC=false) on {model}; {warmup} warm-up calls "
-                       f"({t_warm:.1f} s) + {len(times)} timed, median {t * 1e3:.1f} ms/call")}
+                       f"({t_warm:.1f} s) + {len(times)} timed, median {t * 1e3:.1f} ms/call; value_x_ones: the "
+                       f"reference harness's x = 1.0, 5 timed calls, median {t_ones * 1e3:.1f} ms/call")}
 
 
 def cpu_time_once(A, x_col, k: int, dtype, threads: int, budget_s: float) -> float:
