@@ -1,0 +1,51 @@
+"""bench.py helpers on CPU: the gather-ceiling model, the per-matrix PMC records' engine keying, and
+the dataset summary's aggregates."""
+import json
+import math
+
+import pytest
+
+import bench
+
+
+def test_gather_rate_interpolates_the_probe():
+    for b, r in bench.GATHER_PROBE:
+        assert math.isclose(bench.gather_rate_tbs(b), r, rel_tol=1e-9)
+    assert bench.gather_rate_tbs(1 << 10) == bench.GATHER_PROBE[0][1]          # below the probe: L2-resident rate
+    assert bench.gather_rate_tbs(1 << 40) == bench.GATHER_PROBE[-1][1]         # beyond: the HBM rate
+    mid = bench.gather_rate_tbs(32 << 20)
+    assert bench.GATHER_PROBE[2][1] < mid < bench.GATHER_PROBE[1][1]
+
+
+def test_achievable_takes_the_larger_bound():
+    # config 2 of round 3: 3.13 GB past L2, 34.2 M L2 requests, B of 256 MB, 0.416 ms measured
+    a = bench.achievable(0.41565, 3.131956852e9, 34.18e6, 1e6 * 32 * 8)
+    assert a["bound"] == "past-L2 gather"
+    assert a["t_ms"] == pytest.approx(3.131956852e9 / (bench.gather_rate_tbs(256e6) * 1e12) * 1e3, rel=1e-4)
+    assert a["frac_of_achievable"] == pytest.approx(a["t_ms"] / 0.41565, rel=1e-3)
+    b = bench.achievable(1.0, 1e6, 1e9, 1e6)                   # few past-L2 bytes, many L2 requests
+    assert b["bound"] == "L2 requests" and b["t_l2_ms"] > b["t_past_l2_ms"]
+    assert bench.achievable(1.0, None, None, 1e6) is None
+
+
+def test_pmc_dataset_records_are_keyed_by_engine_build(tmp_path):
+    sha = bench.engine_sha256()
+    recs = [{"gen": "a", "k": 32, "dtype": "f64", "engine_sha256": sha, "traffic_bytes": 1.0},
+            {"gen": "b", "k": 32, "dtype": "f64", "engine_sha256": "0" * 64, "traffic_bytes": 2.0},
+            {"gen": "c", "k": 8, "dtype": "f64", "engine_sha256": sha, "traffic_bytes": 3.0}]
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"engine_sha256": sha, "records": recs}))
+    got = bench.load_pmc_dataset(str(p), 32, "f64")
+    assert set(got) == {"a"}
+    assert bench.load_pmc_dataset(str(tmp_path / "missing.json"), 32, "f64") == {}
+
+
+def test_summarize_aggregates():
+    recs = [{"flops": 2e9, "ms": 1.0, "bytes_alg": 1e9, "frac": 0.125, "gflops": 2000.0, "traffic": 3e9,
+             "frac_of_achievable": 0.5, "cpu_ms": 100.0},
+            {"flops": 6e9, "ms": 1.0, "bytes_alg": 3e9, "frac": 0.375, "gflops": 6000.0}]
+    s = bench.summarize({"recs": recs, "bad": 0, "wall_s": 1.0, "threads": 16, "model": "x"}, 32)
+    assert s["value"] == pytest.approx(4000.0)                 # sum flops / sum time
+    assert s["roofline"]["achieved"] == pytest.approx(2000.0)  # sum bytes / sum time
+    assert s["roofline"]["traffic"] == 3e9 and s["roofline"]["achievable"]["matrices"] == 1
+    assert s["cpu_baseline"]["value"] == pytest.approx(20.0) and "1 of the 2" in s["cpu_baseline"]["sample"]
