@@ -9,13 +9,21 @@ the CPU oracle (bit-exact on the rows the engine reports exact, normwise 1e-10 o
 (bench.engine_sha256); lines already in --out, or whose index is in --done, are skipped, so a sweep resumes across
 gpurun calls (tools/sweep_resumable.sh).  --budget bounds the wall time.
 
+The host side (generation, the inspector's plan per K, the oracle check) costs 10-50x the timed launches, so
+--workers W runs W processes over every W-th line of the work list; each holds an exclusive lock on --gpu-lock
+(flock) from its first warm-up launch to its last timed event, so timed regions never overlap and only host work
+runs in parallel.  A/B of the two modes: re-time lines of an earlier single-process file with the same --stride /
+--offset into another --out and compare the records' ms.
+
   python tools/sweep.py --dataset medium --stride 60 --k 1,8,32,128 --out gpurun_out/sweep_medium.jsonl
 """
 from __future__ import annotations
 
 import argparse
+import fcntl
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -69,7 +77,7 @@ def dataset_lines(args) -> list[str]:
     return lines[args.offset::args.stride]
 
 
-def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, exact):
+def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, exact, gold_rows=64):
     """Oracle on a row sample: sub-CSR of the sampled rows with its columns renumbered, B rows fetched from HBM."""
     import torch
     m = A.m
@@ -91,6 +99,8 @@ def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, exact):
     # the __float128 gold only for the rows that are not exact (exact rows equal the oracle bit for bit, above)
     norm_ok = True
     nx = np.flatnonzero(~seq)
+    if len(nx) > gold_rows:      # the float128 gold is software arithmetic: an evenly spaced subset of them
+        nx = nx[np.linspace(0, len(nx) - 1, gold_rows).round().astype(int)]
     if len(nx):
         srp = np.zeros(len(nx) + 1, np.int32)
         srp[1:] = np.cumsum(np.diff(sub_rp)[nx])
@@ -104,7 +114,7 @@ def sample_parity(S, O, A, B_dev, C_dev, k, nsample, rng, dtype, exact):
             tol = (np.maximum(deg[rows][nx], 1)[:, None] + 1) * 2.0 ** -24 * 1.01
             norm_ok = bool((np.abs(gx.astype(np.float64) - g) <= tol * np.maximum(np.abs(g), absdot)).all())
     return {"rows_checked": int(len(rows)), "bitexact_seq_rows": bit_ok, "normwise_ok": norm_ok,
-            "long_rows_checked": int((~seq).sum())}
+            "long_rows_checked": int(len(nx))}
 
 
 def cpu_baseline(O, A, vals, x_col, k, budget_s, cores):
@@ -133,6 +143,24 @@ def cpu_baseline(O, A, vals, x_col, k, budget_s, cores):
             "cpu_cores": cores}
 
 
+def spawn_workers(args) -> int:
+    """Run --workers copies of this sweep over interleaved slices of the work list, one output file each
+    (<out stem>.w<i>.jsonl: tools/sweep_merge.py folds them), sharing one GPU lock; exit with the worst status."""
+    out = Path(args.out)
+    lock = args.gpu_lock or str(out.with_suffix(".gpulock"))
+    argv = [a for a in sys.argv[1:]]
+    procs = []
+    for i in range(args.workers):
+        wout = out.with_name(f"{out.stem}.w{i}{out.suffix}")
+        cmd = [sys.executable, "-u", __file__, *argv, "--worker", f"{i}/{args.workers}", "--gpu-lock", lock,
+               "--out", str(wout)]
+        procs.append(subprocess.Popen(cmd, stdout=open(wout.with_suffix(".log"), "a"), stderr=subprocess.STDOUT))
+    rcs = [p.wait() for p in procs]
+    for i, rc in enumerate(rcs):
+        print(f"worker {i}: exit {rc}", flush=True)
+    return max(rcs, key=abs)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="medium",
@@ -154,8 +182,14 @@ def main():
     ap.add_argument("--budget", type=float, default=1e9, help="seconds; stop starting new matrices after this")
     ap.add_argument("--done", default=None, help="file of dataset line indices already swept (skipped)")
     ap.add_argument("--no-features", action="store_true", help="skip the per-matrix feature extraction")
+    ap.add_argument("--gold-rows", type=int, default=64, help="inexact sampled rows checked against the fp128 gold")
+    ap.add_argument("--workers", type=int, default=1, help="host worker processes (timed regions serialised)")
+    ap.add_argument("--worker", default=None, help=argparse.SUPPRESS)     # i/W: set by --workers
+    ap.add_argument("--gpu-lock", default=None, help="lock file serialising the timed regions of the workers")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "sweep.jsonl"))
     args = ap.parse_args()
+    if args.workers > 1 and args.worker is None:
+        return spawn_workers(args)
 
     from concurrent.futures import ThreadPoolExecutor
     import torch
@@ -199,6 +233,10 @@ def main():
         if p.nr_rows * p.avg_nnz_per_row > args.max_nnz:
             continue
         work.append((idx, line, todo))
+    if args.worker is not None:
+        wi_, wn_ = (int(x) for x in args.worker.split("/"))
+        work = work[wi_::wn_]
+    lock_f = open(args.gpu_lock, "a+") if args.gpu_lock else None
 
     def prepare(line):
         t0 = time.time()
@@ -213,22 +251,31 @@ def main():
         if time.time() - t_start > args.budget:
             print(f"budget reached after {wi} lines", flush=True)
             break
+        tw = time.time()
         A, t_gen, feat = fut.result()
+        t_wait = time.time() - tw
         fut = ex.submit(prepare, work[wi + 1][1]) if wi + 1 < len(work) else None
         for dt in dtypes:
             dtype = np.float64 if dt == "f64" else np.float32
             tdtype = torch.float64 if dt == "f64" else torch.float32
             vals = A.values.astype(dtype)
+            tc = time.time()
             mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
+            t_create = time.time() - tc
             for dt2, k in todo:
                 if dt2 != dt:
                     continue
+                t0 = time.time()
                 mf.plan(k)
+                t_plan = time.time() - t0
                 g = torch.Generator(device=dev)
                 g.manual_seed(42)
                 B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
                 Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
                 run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
+                torch.cuda.synchronize()
+                if lock_f:
+                    fcntl.flock(lock_f, fcntl.LOCK_EX)
                 for _ in range(args.warmup):
                     run()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -237,9 +284,14 @@ def main():
                     run()
                 e1.record(stream)
                 torch.cuda.synchronize()
+                if lock_f:
+                    fcntl.flock(lock_f, fcntl.LOCK_UN)
                 ms = e0.elapsed_time(e1) / args.iters
+                t_timed = time.time() - t0 - t_plan
                 bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
-                par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows())
+                t1 = time.time()
+                par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows(), args.gold_rows)
+                t_check = time.time() - t1
                 inf = mf.info()
                 rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
                        "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
@@ -248,6 +300,8 @@ def main():
                        "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
                        "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
                        "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
+                       "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
+                                  "timed": round(t_timed, 3), "check": round(t_check, 3)},
                        **par}
                 if feat is not None:
                     rec["mem_mb"] = feat["mem_footprint"]
@@ -269,4 +323,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
