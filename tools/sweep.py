@@ -175,6 +175,9 @@ def main():
     ap.add_argument("--dtype", default="f64", help="comma list of f64,f32")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--batches", type=int, default=1,
+                    help="timed batches of --iters launches; ms = the lowest batch mean (3 with --workers: another "
+                         "worker's allocations and uploads can stall a batch even though timed regions never overlap)")
     ap.add_argument("--check-rows", type=int, default=256)
     ap.add_argument("--max-nnz", type=float, default=2.0e8)
     ap.add_argument("--cpu-baseline", type=float, default=0.0,
@@ -190,6 +193,8 @@ def main():
     args = ap.parse_args()
     if args.workers > 1 and args.worker is None:
         return spawn_workers(args)
+    if args.worker is not None and "--batches" not in sys.argv:
+        args.batches = 3
 
     from concurrent.futures import ThreadPoolExecutor
     import torch
@@ -255,71 +260,88 @@ def main():
         A, t_gen, feat = fut.result()
         t_wait = time.time() - tw
         fut = ex.submit(prepare, work[wi + 1][1]) if wi + 1 < len(work) else None
-        for dt in dtypes:
-            dtype = np.float64 if dt == "f64" else np.float32
-            tdtype = torch.float64 if dt == "f64" else torch.float32
-            vals = A.values.astype(dtype)
-            tc = time.time()
-            mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
-            t_create = time.time() - tc
-            for dt2, k in todo:
-                if dt2 != dt:
-                    continue
-                t0 = time.time()
-                mf.plan(k)
-                t_plan = time.time() - t0
-                g = torch.Generator(device=dev)
-                g.manual_seed(42)
-                B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
-                Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
-                run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
-                torch.cuda.synchronize()
-                if lock_f:
-                    fcntl.flock(lock_f, fcntl.LOCK_EX)
-                for _ in range(args.warmup):
-                    run()
+        try:
+            sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock_f, idx, line, todo, A, t_gen,
+                       t_wait, feat, dtypes)
+        except (S.SpmmHipError, torch.OutOfMemoryError) as e:     # e.g. device memory held by other workers
+            if lock_f:
+                fcntl.flock(lock_f, fcntl.LOCK_UN)
+            print(f"line {idx} skipped: {e}", flush=True)
+        del A
+        if args.worker is not None:
+            torch.cuda.empty_cache()
+    ex.shutdown(cancel_futures=True)
+
+
+def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock_f, idx, line, todo, A, t_gen, t_wait,
+               feat, dtypes):
+    """Every requested (dtype, K) of one generated matrix: plan, time, check, append one record each."""
+    for dt in dtypes:
+        dtype = np.float64 if dt == "f64" else np.float32
+        tdtype = torch.float64 if dt == "f64" else torch.float32
+        vals = A.values.astype(dtype)
+        tc = time.time()
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
+        t_create = time.time() - tc
+        for dt2, k in todo:
+            if dt2 != dt:
+                continue
+            t0 = time.time()
+            mf.plan(k)
+            t_plan = time.time() - t0
+            g = torch.Generator(device=dev)
+            g.manual_seed(42)
+            B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
+            Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
+            run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
+            torch.cuda.synchronize()
+            if lock_f:
+                fcntl.flock(lock_f, fcntl.LOCK_EX)
+            for _ in range(args.warmup):
+                run()
+            ms_b = []
+            for _ in range(args.batches):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(args.iters):
                     run()
                 e1.record(stream)
                 torch.cuda.synchronize()
-                if lock_f:
-                    fcntl.flock(lock_f, fcntl.LOCK_UN)
-                ms = e0.elapsed_time(e1) / args.iters
-                t_timed = time.time() - t0 - t_plan
-                bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
-                t1 = time.time()
-                par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows(), args.gold_rows)
-                t_check = time.time() - t1
-                inf = mf.info()
-                rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
-                       "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
-                       "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9, "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12,
-                       "engine_sha256": sha, "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
-                       "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
-                       "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
-                       "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
-                       "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
-                                  "timed": round(t_timed, 3), "check": round(t_check, 3)},
-                       **par}
-                if feat is not None:
-                    rec["mem_mb"] = feat["mem_footprint"]
-                    rec["features"] = {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled",
-                                                            "skew", "avg_num_neighbours", "cross_row_similarity")}
-                if args.cpu_baseline > 0:
-                    x_col = np.ascontiguousarray(B.cpu().numpy().T).ravel()
-                    rec.update(cpu_baseline(O, A, vals, x_col, k, args.cpu_baseline, cores))
-                    rec["gpu_over_cpu"] = rec["gflops"] / rec["cpu_gflops"]
-                with open(out, "a") as f:
-                    f.write(json.dumps(rec) + "\n")
-                print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
-                                                             "roofline_frac", "cpu_gflops", "bitexact_seq_rows",
-                                                             "normwise_ok")}), flush=True)
-                del B, Cm
-            mf.close()
-        del A
-    ex.shutdown(cancel_futures=True)
+                ms_b.append(e0.elapsed_time(e1) / args.iters)
+            if lock_f:
+                fcntl.flock(lock_f, fcntl.LOCK_UN)
+            ms = min(ms_b)
+            t_timed = time.time() - t0 - t_plan
+            bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
+            t1 = time.time()
+            par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows(), args.gold_rows)
+            t_check = time.time() - t1
+            inf = mf.info()
+            rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
+                   "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
+                   "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9, "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12,
+                   "engine_sha256": sha, "batches": [round(x, 5) for x in ms_b], "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
+                   "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
+                   "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
+                   "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
+                   "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
+                              "timed": round(t_timed, 3), "check": round(t_check, 3)},
+                   **par}
+            if feat is not None:
+                rec["mem_mb"] = feat["mem_footprint"]
+                rec["features"] = {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled",
+                                                        "skew", "avg_num_neighbours", "cross_row_similarity")}
+            if args.cpu_baseline > 0:
+                x_col = np.ascontiguousarray(B.cpu().numpy().T).ravel()
+                rec.update(cpu_baseline(O, A, vals, x_col, k, args.cpu_baseline, cores))
+                rec["gpu_over_cpu"] = rec["gflops"] / rec["cpu_gflops"]
+            with open(out, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+            print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
+                                                         "roofline_frac", "cpu_gflops", "bitexact_seq_rows",
+                                                         "normwise_ok")}), flush=True)
+            del B, Cm
+        mf.close()
 
 
 if __name__ == "__main__":
