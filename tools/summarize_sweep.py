@@ -94,6 +94,20 @@ def table(recs, k, title):
     return "\n".join(out) + "\n"
 
 
+def size_table(recs, k, title):
+    """Per nnz bin at one K: the launch-latency-bound small matrices next to the bandwidth-bound large ones."""
+    bins = [(0, 1e6, "< 1 M"), (1e6, 4e6, "1-4 M"), (4e6, 16e6, "4-16 M"), (16e6, 64e6, "16-64 M"),
+            (64e6, 1e12, ">= 64 M")]
+    out = [f"#### {title}: K = {k} by matrix size", "",
+           "| nonzeros | | matrices | median frac | p10 | p90 | median GFLOP/s | aggregate GFLOP/s | aggregate alg. GB/s |",
+           "|---|---|---|---|---|---|---|---|---|"]
+    for lo, hi, name in bins:
+        rs = [r for r in recs if r["k"] == k and lo <= r["nnz"] < hi]
+        if rs:
+            out.append(row_line(name, "", rs))
+    return "\n".join(out) + "\n"
+
+
 def row_line(a, b, rs):
     fr = np.array([r["roofline_frac"] for r in rs])
     gf = np.array([r["gflops"] for r in rs])
@@ -123,6 +137,8 @@ def main():
           f"engine builds: " + ", ".join(f"{k} ({v} records)" for k, v in shas.most_common()) + "\n")
     for k in (int(x) for x in args.k.split(",")):
         print(table(recs, k, args.title))
+    for k in (int(x) for x in args.k.split(",")):
+        print(size_table(recs, k, args.title))
     if args.pmc:
         print(achievable_table(args.pmc, args.engine))
 
