@@ -14,11 +14,11 @@ LIB = ROOT / "spmm-research_amd" / "lib"
 def declared(header: str) -> list[str]:
     text = (ROOT / "include" / header).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(spmm_(?:hip|host|sddmm)_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(spmm_(?:hip|host|sddmm|pbv)_[a-z0-9_]+)\s*\(", text)))
 
 
 @pytest.mark.parametrize("header,lib", [("spmm_hip.h", "libspmm_hip.so"), ("spmm_host.h", "libspmm_host.so"),
-                                        ("spmm_pipeline.h", "libspmm_hip.so")])
+                                        ("spmm_pipeline.h", "libspmm_hip.so"), ("spmm_pbv.h", "libspmm_pbv.so")])
 def test_exports_every_declared_symbol(header, lib):
     names = declared(header)
     assert len(names) >= (4 if header == "spmm_pipeline.h" else 10)
