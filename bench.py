@@ -164,7 +164,7 @@ def engine_sha256() -> str:
     h = hashlib.sha256()
     pkg = ROOT / "spmm-research_amd"
     for f in (pkg / "csrc" / "spmm_engine.hip", pkg / "csrc" / "spmm_kernels.hpp", pkg / "csrc" / "spmm_handle.hpp",
-              pkg / "csrc" / "spmm_multi.hip", ROOT / "include" / "spmm_hip.h", pkg / "Makefile"):
+              pkg / "csrc" / "spmm_multi.hip", pkg / "csrc" / "spmm_mfma.hpp", ROOT / "include" / "spmm_hip.h", pkg / "Makefile"):
         h.update(f.read_bytes())
     return h.hexdigest()
 

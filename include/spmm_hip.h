@@ -152,6 +152,11 @@ int spmm_hip_info(const spmm_hip_t *h, int64_t *out);
  * out[6]=the tile kernel's compute-lane width in 16-byte pieces of a B row (1, 2, 4; SPMM_HIP_TILE_WIDE=<S>).
  * SPMM_HIP_TILES=-1 disables tiles, =1 takes every eligible tile; SPMM_HIP_TILE_REUSE=<x> sets the threshold. */
 int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out);
+/* Which kernel runs the tiles of the current plan: 0 = no tiles, 1 = the sparse LDS tile kernel (spmm_tile_kernel),
+ * 2 = matrix-core tiles (spmm_mfma_tile_kernel, DESIGN.md §3.9: fp64 32-column panels, 16-row tiles multiplied as
+ * dense panels by v_mfma_f64_16x16x4_f64 -- the f64 MFMA is a chain of fused multiply-adds in k order, so these rows
+ * are exact too).  SPMM_HIP_MFMA=-1 keeps the sparse tile kernel, 1 takes every eligible 16-row tile. */
+int spmm_hip_tile_mode(const spmm_hip_t *h);
 
 /* Which C rows of the current plan are computed as ONE left-to-right FMA chain over the row in CSR order -- the
  * reference kernel's exact operation sequence, so bit-identical to it (mask[i] = 1); the others (rows longer than

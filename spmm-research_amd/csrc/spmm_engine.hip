@@ -33,6 +33,7 @@
 #include "../../include/spmm_hip.h"
 #include "spmm_handle.hpp"
 #include "spmm_kernels.hpp"
+#include "spmm_mfma.hpp"
 
 using namespace spmm;
 using namespace spmm_engine;
@@ -78,6 +79,11 @@ constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgr
 constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
 constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value +0, the zero B row)
 constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
+// Matrix-core tiles (spmm_mfma_tile_kernel): fp64, 32-column panels, rows with strictly increasing
+// columns, B below 4 GiB (32-bit buffer offsets).  Policy: sampled reuse of 16-row tiles (nonzeros per union column;
+// reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE and enough tiles to fill the chip.
+constexpr double MFMA_MIN_REUSE = 2.0;
+constexpr int64_t MFMA_MIN_TILES = 1024;
 
 int pow2_ceil(int64_t x) {
     int p = 1;
@@ -276,6 +282,19 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
     }
 }
 
+// Matrix-core tiles for a 32-column fp64 panel: four 16-row tiles (one per wave) per workgroup.
+// B and C point at the panel's first column; the buffer descriptor of B covers the rest of the array.
+void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, hipStream_t s) {
+    const int grid = (h->plan.ntile + 3) / 4;
+    const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)k0) * sizeof(double));
+    if (h->plan.tile_xcd)
+        spmm_mfma_tile_kernel<true><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
+                                                        (const double *)h->d_tval, h->d_tlidx, B, bb, C, ld);
+    else
+        spmm_mfma_tile_kernel<false><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
+                                                         (const double *)h->d_tval, h->d_tlidx, B, bb, C, ld);
+}
+
 template <typename T>
 void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     T *P = (T *)h->d_part;
@@ -283,7 +302,15 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
         if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
-        if (h->plan.ntile > 0) launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
+        if (h->plan.ntile > 0) {
+            if constexpr (std::is_same_v<T, double>) {
+                if (h->plan.tile_mfma) {
+                    launch_mfma(h, B + k0, C + k0, K, k0, s);
+                    continue;
+                }
+            }
+            launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
+        }
     }
     if (h->nlong > 0 && !h->fuse) {
         spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
@@ -450,6 +477,13 @@ bool rows_sorted(const int32_t *rp, const int32_t *col, int64_t m) {
     for (int64_t r = 0; r < m; ++r)
         for (int64_t j = (int64_t)rp[r] + 1; j < rp[r + 1]; ++j)
             if (col[j] < col[j - 1]) return false;
+    return true;
+}
+// every row's columns strictly increasing (no repeated column: one panel cell per entry)
+bool rows_strict(const int32_t *rp, const int32_t *col, int64_t m) {
+    for (int64_t r = 0; r < m; ++r)
+        for (int64_t j = (int64_t)rp[r] + 1; j < rp[r + 1]; ++j)
+            if (col[j] <= col[j - 1]) return false;
     return true;
 }
 
@@ -1123,7 +1157,29 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         const int64_t win_forced = h->var.win_bytes != 0 ? h->var.win_bytes : (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
         if (forced >= 0 && shape_ok && win_forced <= 0) {
             if (int st = load_cols()) return st;
-            if (rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
+            // matrix-core tiles first: fp64 32-column panels, strictly increasing columns, B < 4 GiB
+            const int env_m = env_int("SPMM_HIP_MFMA", 0);
+            const int fm = h->var.mfma != 0 ? h->var.mfma : env_m;
+            const bool mshape = h->vsize == 8 && pl.kw == 32 && k % 32 == 0 &&
+                                (double)h->ncols * (double)k * 8.0 < 4294967296.0;
+            if (fm >= 0 && mshape && rows_strict(h->h_row_ptr.data(), hcol.data(), h->m)) {
+                const char *mthr = getenv("SPMM_HIP_MFMA_REUSE");
+                const double mreuse = (mthr && *mthr) ? atof(mthr) : (forced > 0 || fm > 0) ? 1.0 : MFMA_MIN_REUSE;
+                const double r16 = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max,
+                                                     MFMA_ROWS);
+                const bool menough = (h->m + MFMA_ROWS - 1) / MFMA_ROWS >= MFMA_MIN_TILES;
+                if (forced > 0 || fm > 0 || (menough && r16 >= mreuse)) {
+                    tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, MFMA_ROWS,
+                                        MFMA_UC, MFMA_CAPA, mreuse, tp);
+                    if (tiles && forced <= 0 && fm <= 0 && (int64_t)tp.tiles.size() < MFMA_MIN_TILES / 2) tiles = false;
+                    if (tiles && !tile_tables_fit(tp)) tiles = false;
+                    if (tiles) {
+                        pl.tile_mfma = 1;
+                        pl.tile_reuse = r16;
+                    }
+                }
+            }
+            if (!tiles && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
                 const int rows_env = env_int("SPMM_HIP_TILE_ROWS", 0);
                 int rmax = std::min((WG / g_t) * tile_rpg(g_t), rows_env > 0 ? rows_env : TILE_ROWS);
                 const char *thr = getenv("SPMM_HIP_TILE_REUSE");
@@ -1335,7 +1391,43 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         if (e == hipSuccess) e = alloc_copy((void **)&h->d_wperm, wp.data(), wp.size() * 4);
         h->insp_bytes += wcol.size() * 4 + wval.size();
     }
-    if (e == hipSuccess && tiles) {
+    if (e == hipSuccess && tiles && pl.tile_mfma) {
+        std::vector<char> hval((size_t)h->nnz * h->vsize);
+        e = hipMemcpy(hval.data(), h->d_val, hval.size(), hipMemcpyDeviceToHost);
+        const size_t nz = tp.perm.size();
+        std::vector<char> tval(nz * h->vsize + PAD_BYTES, 0);
+        for (size_t q = 0; q < nz; ++q)
+            if (tp.perm[q] >= 0) std::memcpy(&tval[q * h->vsize], &hval[(size_t)tp.perm[q] * h->vsize], h->vsize);
+        {
+            // matrix-core tables: each entry's panel cell (row in tile * PST + chunk column; padding -> the trash
+            // cell) and each chunk's union columns in [g][k step] order, 48 slots, padded with a valid row
+            const int64_t nch = (int64_t)tp.chunks.size() - 1;
+            std::vector<uint16_t> cell(nz + PAD_BYTES / 2, (uint16_t)MFMA_TRASH);
+            std::vector<int32_t> tcolT((size_t)nch * MFMA_UC + PAD_BYTES / 4, 0);
+            for (const int4 &t : tp.tiles)
+                for (int ci = t.z; ci < t.z + t.w; ++ci) {
+                    const int4 ch = tp.chunks[(size_t)ci];
+                    for (int q = 0; q < t.y; ++q)
+                        for (int p = tp.tseg[(size_t)ch.w + q]; p < tp.tseg[(size_t)ch.w + q + 1]; ++p) {
+                            const uint16_t lc = tp.tlidx[(size_t)ch.z + p];
+                            if (lc != TILE_PAD_LIDX) cell[(size_t)ch.z + p] = (uint16_t)(q * MFMA_PST + lc);
+                        }
+                    for (int u = 0; u < MFMA_UC; ++u)
+                        tcolT[(size_t)ci * MFMA_UC + (u % 4) * MFMA_KS + u / 4] = tp.tcol[(size_t)ch.x + std::min(u, ch.y - 1)];
+                }
+            if (e == hipSuccess) e = alloc_copy((void **)&h->d_tiles, tp.tiles.data(), tp.tiles.size() * sizeof(int4));
+            if (e == hipSuccess) e = alloc_copy((void **)&h->d_tchunk, tp.chunks.data(), tp.chunks.size() * sizeof(int4));
+            if (e == hipSuccess) e = alloc_copy((void **)&h->d_tcol, tcolT.data(), tcolT.size() * 4);
+            if (e == hipSuccess) e = alloc_copy((void **)&h->d_tlidx, cell.data(), cell.size() * 2);
+            if (e == hipSuccess) e = alloc_copy(&h->d_tval, tval.data(), tval.size());
+            std::vector<int32_t> tpm(tp.perm.begin(), tp.perm.end());
+            h->ntperm = (int64_t)tpm.size();
+            if (e == hipSuccess) e = alloc_copy((void **)&h->d_tperm, tpm.data(), tpm.size() * 4);
+            h->insp_bytes += tp.tiles.size() * sizeof(int4) + tp.chunks.size() * sizeof(int4) + tcolT.size() * 4 +
+                             cell.size() * 2 + tval.size() + tpm.size() * 4;
+        }
+    }
+    if (e == hipSuccess && tiles && !pl.tile_mfma) {
         // chunk-major copies of the tile rows' values and their chunk-local column indices (+ 64 B of padding)
         std::vector<char> hval((size_t)h->nnz * h->vsize);
         e = hipMemcpy(hval.data(), h->d_val, hval.size(), hipMemcpyDeviceToHost);
@@ -1708,6 +1800,12 @@ int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out) {
     out[5] = h->plan.tile_xcd;
     out[6] = h->plan.tile_wide;
     return SPMM_HIP_OK;
+}
+
+int spmm_hip_tile_mode(const spmm_hip_t *h) {
+    if (!h) return fail(SPMM_HIP_ERR_ARG, "tile_mode: bad handle");
+    if (h->multi) return 0;
+    return h->plan.ntile == 0 ? 0 : h->plan.tile_mfma ? 2 : 1;
 }
 
 int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask) {

@@ -45,6 +45,7 @@ struct Plan {
     int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
     int tile_xcd = 0;          // tiles in XCD-contiguous order
     int tile_wide = 1;         // compute-lane width in 16-byte pieces of a B row (1, 2, 4), where RPG allows
+    int tile_mfma = 0;         // 1 = the tiles run on the matrix cores (spmm_mfma_tile_kernel, 16-row wave tiles)
     int64_t tile_rows = 0, tile_nnz = 0, tile_chunks = 0;
     double tile_reuse = 0.0;   // sampled mean reuse (nnz per union column) the policy saw
 };
@@ -57,6 +58,7 @@ struct Variant {
     int xcd = 0;               // 0 = inspector policy, < 0 = off, > 0 = XCD-contiguous block order
     int lanes = 0;             // 0 = inspector policy, < 0 = off (exact rows), > 0 = vector lanes up to this many
     int tiles = 0;             // 0 = inspector policy, < 0 = off, > 0 = every eligible tile with reuse >= 1
+    int mfma = 0;              // 0 = inspector policy, < 0 = sparse LDS tiles only, > 0 = matrix-core tiles when eligible
 };
 
 struct MultiState;                              // spmm_multi.hip
@@ -102,9 +104,9 @@ struct spmm_hip_handle {
     bool fuse = false;               // split rows combined inside the row kernel (no spmm_combine_kernel launch)
     int32_t *d_wcol = nullptr;       // chained mode: col_idx / values in window-major segment order
     void *d_wval = nullptr;
-    int4 *d_tiles = nullptr, *d_tchunk = nullptr;   // tile mode (spmm_tile_kernel)
-    int32_t *d_tcol = nullptr;
-    uint16_t *d_tseg = nullptr, *d_tlidx = nullptr;
+    int4 *d_tiles = nullptr, *d_tchunk = nullptr;   // tile mode (spmm_tile_kernel / spmm_mfma_tile_kernel)
+    int32_t *d_tcol = nullptr;       // union columns (matrix-core tiles: per chunk 48 slots in [g][k step] order)
+    uint16_t *d_tseg = nullptr, *d_tlidx = nullptr;  // (matrix-core tiles: d_tlidx = panel cells)
     void *d_tval = nullptr;
     long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
     int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)

@@ -123,7 +123,8 @@ def test_pipeline_device_path_and_graph(env, dtype):
     pipe.close()
 
 
-@pytest.mark.parametrize("force", [{"SPMM_HIP_TILES": "1"}, {"SPMM_HIP_WIN_BYTES": "4096"}, {}])
+@pytest.mark.parametrize("force", [{"SPMM_HIP_TILES": "1"}, {"SPMM_HIP_TILES": "1", "SPMM_HIP_MFMA": "-1"},
+                                   {"SPMM_HIP_WIN_BYTES": "4096"}, {}])
 def test_update_values_regathers(env, monkeypatch, force):
     """New values through spmm_hip_update_values[_device] == a handle built with them, also when the plan keeps
     window-major (chained) or tile (chunk-major) copies of the values."""

@@ -21,6 +21,13 @@ def env():
     return torch, S, O
 
 
+@pytest.fixture(autouse=True)
+def sparse_tile_kernel(monkeypatch):
+    """These tests cover the sparse LDS tile kernel; fp64 32-column panels would otherwise take the matrix-core tile
+    kernel (tests/test_gpu_mfma.py)."""
+    monkeypatch.setenv("SPMM_HIP_MFMA", "-1")
+
+
 def bits(a):
     a = np.ascontiguousarray(a)
     return a.view(np.int64 if a.dtype == np.float64 else np.int32)

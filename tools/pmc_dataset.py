@@ -33,7 +33,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 sys.path.insert(0, str(ROOT))
-ENGINE = ("spmm_rows_kernel", "spmm_tile_kernel", "spmm_combine_kernel")
+ENGINE = ("spmm_rows_kernel", "spmm_tile_kernel", "spmm_mfma_tile_kernel", "spmm_combine_kernel")
 PASSES = [["FETCH_SIZE"], ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]]
 
 
