@@ -83,6 +83,10 @@ constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding 
 // columns, B below 4 GiB (32-bit buffer offsets).  Policy: sampled reuse of 16-row tiles (nonzeros per union column;
 // reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE and enough tiles to fill the chip.
 constexpr double MFMA_MIN_REUSE = 2.0;
+// Leftover rows of a plan whose tiles hold more than 1 - GAP_SHORT_FRAC of the nonzeros run as pieces of at most
+// GAP_SEQ_MAX nonzeros (a lone long row would otherwise be a serial straggler after the tile kernel).
+constexpr double GAP_SHORT_FRAC = 0.125;
+constexpr int GAP_SEQ_MAX = 64;
 constexpr int64_t MFMA_MIN_TILES = 1024;
 
 int pow2_ceil(int64_t x) {
@@ -284,15 +288,19 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
 
 // Matrix-core tiles for a 32-column fp64 panel: four 16-row tiles (one per wave) per workgroup.
 // B and C point at the panel's first column; the buffer descriptor of B covers the rest of the array.
-void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, hipStream_t s) {
+void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, int kw, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
-    const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)k0) * sizeof(double));
-    if (h->plan.tile_xcd)
-        spmm_mfma_tile_kernel<true><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
-                                                        (const double *)h->d_tval, h->d_tlidx, B, bb, C, ld);
-    else
-        spmm_mfma_tile_kernel<false><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
-                                                         (const double *)h->d_tval, h->d_tlidx, B, bb, C, ld);
+    for (int k1 = 0; k1 + 32 <= kw; k1 += 32) {            // the kernel covers 32 columns: sub-panels of this panel
+        const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)(k0 + k1)) * sizeof(double));
+        if (h->plan.tile_xcd)
+            spmm_mfma_tile_kernel<true><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
+                                                            (const double *)h->d_tval, h->d_tlidx, B + k1, bb,
+                                                            C + k1, ld);
+        else
+            spmm_mfma_tile_kernel<false><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
+                                                             (const double *)h->d_tval, h->d_tlidx, B + k1, bb,
+                                                             C + k1, ld);
+    }
 }
 
 template <typename T>
@@ -305,7 +313,7 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         if (h->plan.ntile > 0) {
             if constexpr (std::is_same_v<T, double>) {
                 if (h->plan.tile_mfma) {
-                    launch_mfma(h, B + k0, C + k0, K, k0, s);
+                    launch_mfma(h, B + k0, C + k0, K, k0, kw, s);
                     continue;
                 }
             }
@@ -1155,14 +1163,14 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                               pow2_ceil(srow / 16) == srow / 16 &&
                               h->ncols < INT32_MAX;
         const int64_t win_forced = h->var.win_bytes != 0 ? h->var.win_bytes : (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
-        if (forced >= 0 && shape_ok && win_forced <= 0) {
+        // matrix-core tiles first: fp64 32-column panels, strictly increasing columns, B < 4 GiB
+        const int env_m = env_int("SPMM_HIP_MFMA", 0);
+        const int fm = h->var.mfma != 0 ? h->var.mfma : env_m;
+        const bool mshape = fm >= 0 && h->vsize == 8 && pl.kw % 32 == 0 && k % 32 == 0 &&
+                            (double)h->ncols * (double)k * 8.0 < 4294967296.0;
+        if (forced >= 0 && h->nnz > 0 && h->ncols < INT32_MAX && win_forced <= 0 && (mshape || shape_ok)) {
             if (int st = load_cols()) return st;
-            // matrix-core tiles first: fp64 32-column panels, strictly increasing columns, B < 4 GiB
-            const int env_m = env_int("SPMM_HIP_MFMA", 0);
-            const int fm = h->var.mfma != 0 ? h->var.mfma : env_m;
-            const bool mshape = h->vsize == 8 && pl.kw == 32 && k % 32 == 0 &&
-                                (double)h->ncols * (double)k * 8.0 < 4294967296.0;
-            if (fm >= 0 && mshape && rows_strict(h->h_row_ptr.data(), hcol.data(), h->m)) {
+            if (mshape && rows_strict(h->h_row_ptr.data(), hcol.data(), h->m)) {
                 const char *mthr = getenv("SPMM_HIP_MFMA_REUSE");
                 const double mreuse = (mthr && *mthr) ? atof(mthr) : (forced > 0 || fm > 0) ? 1.0 : MFMA_MIN_REUSE;
                 const double r16 = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max,
@@ -1179,7 +1187,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                     }
                 }
             }
-            if (!tiles && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
+            if (!tiles && shape_ok && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
                 const int rows_env = env_int("SPMM_HIP_TILE_ROWS", 0);
                 int rmax = std::min((WG / g_t) * tile_rpg(g_t), rows_env > 0 ? rows_env : TILE_ROWS);
                 const char *thr = getenv("SPMM_HIP_TILE_REUSE");
@@ -1240,6 +1248,12 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         pl.nwin = (int)in.win_blk.size() - 1;
         pl.nseg = (int64_t)in.vdest.size();
     } else {
+        // when tiles hold nearly all the work, the row kernel's launch is only the leftover rows -- typically one
+        // skewed row of thousands of nonzeros whose T-pieces each run as a latency-bound serial chain (~64 us for
+        // 2,048 gathers) after the tile kernel: cut those rows into short pieces instead
+        if (tiles && pl.tile_mfma && (double)(h->nnz - tp.nnz) < GAP_SHORT_FRAC * (double)h->nnz && pl.seq_max > GAP_SEQ_MAX &&
+            h->var.seq_max <= 0 && env_int("SPMM_HIP_SEQ_MAX", 0) <= 0)
+            pl.seq_max = GAP_SEQ_MAX;
         inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd,
                 tiles ? tp.in_tile.data() : nullptr, pl.block_rows);
         pl.nseg = (int64_t)in.vrow_ptr.size() - 1;

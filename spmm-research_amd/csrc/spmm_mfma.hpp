@@ -48,8 +48,8 @@ constexpr int MFMA_PSZ = MFMA_TRASH + 2;       // one wave's panel (+ trash cell
 constexpr int MFMA_CAPA = 512;                 // entries per chunk (8 per lane)
 constexpr int MFMA_NPE = MFMA_CAPA / 64;
 
-template <bool XCD, int V = 0>
-__global__ __launch_bounds__(256, V == 1 ? 2 : 3) void spmm_mfma_tile_kernel(const int4 *__restrict__ tiles, int ntiles,
+template <bool XCD>
+__global__ __launch_bounds__(256, 3) void spmm_mfma_tile_kernel(const int4 *__restrict__ tiles, int ntiles,
                                                                const int4 *__restrict__ tchunk,
                                                                const int32_t *__restrict__ tcolT,
                                                                const double *__restrict__ tval,
@@ -132,117 +132,42 @@ __global__ __launch_bounds__(256, V == 1 ? 2 : 3) void spmm_mfma_tile_kernel(con
         for (int i = 0; i < 4; ++i) acc0[i] = x[i], acc1[i] = x[4 + i];
     };
 
-    if constexpr (V == 0) {
-        // prologue: chunk 0 in the panel, B operand of chunk 0, entries and union columns of chunk 1
-        load_tcol(0);
-    #pragma unroll
-        for (int st = 0; st < MFMA_KS; ++st) load_b1(st);
-        load_e(0);
-        scatter();
-        load_e(min(1, tl.w - 1));
-        load_tcol(min(1, tl.w - 1));
-        for (int c = 0; c < tl.w; ++c) {
-            const int ns = (tchunk[tl.z + c].y + 3) >> 2;
-            double a[MFMA_KS];
-            const double *pa = P + (l & 15) * MFMA_PST + g;
-    #pragma unroll
-            for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
-    #pragma unroll
-            for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = 0.0;
-            if (c + 1 < tl.w) scatter();
-            load_e(min(c + 2, tl.w - 1));
-            const f64x4 s0 = acc0, s1 = acc1;
-    #pragma unroll
-            for (int st = 0; st < MFMA_KS; ++st) {
-                if (st < ns) {
-                    double bb[2];
-                    __builtin_memcpy(bb, &bo[st], 16);
-                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[0], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[1], acc1, 0, 0, 0);
-                }
-                load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
-            }
-            load_tcol(min(c + 2, tl.w - 1));
-            bool bad = false;
-    #pragma unroll
-            for (int i = 0; i < 4; ++i) bad |= !__builtin_isfinite(acc0[i]) || !__builtin_isfinite(acc1[i]);
-            if (__builtin_amdgcn_ballot_w64(bad)) {
-                acc0 = s0, acc1 = s1;
-                sparse_chunk(c);
-            }
-        }
-    } else {
-        // V = 1: entries three chunks ahead in two register sets; Inf/NaN found in the B operand before the MFMAs
-        struct Ents {
-            double v[MFMA_NPE];
-            int p[MFMA_NPE];
-            int n;
-        };
-        auto load_e2 = [&](Ents &E, int c) {
-            const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
-            E.n = cn.z - ch.z;
+    // prologue: chunk 0 in the panel, B operand of chunk 0, entries and union columns of chunk 1
+    load_tcol(0);
 #pragma unroll
-            for (int j = 0; j < MFMA_NPE; ++j) {
-                const int e = min(j * 64 + l, E.n - 1);
-                E.v[j] = __builtin_nontemporal_load(tval + ch.z + e);
-                E.p[j] = (int)__builtin_nontemporal_load(tpos + ch.z + e);
-            }
-        };
-        auto scatter2 = [&](const Ents &E) {
+    for (int st = 0; st < MFMA_KS; ++st) load_b1(st);
+    load_e(0);
+    scatter();
+    load_e(min(1, tl.w - 1));
+    load_tcol(min(1, tl.w - 1));
+    for (int c = 0; c < tl.w; ++c) {
+        const int ns = (tchunk[tl.z + c].y + 3) >> 2;
+        double a[MFMA_KS];
+        const double *pa = P + (l & 15) * MFMA_PST + g;
 #pragma unroll
-            for (int j = 0; j < MFMA_NPE; ++j) {
-                const int cell = j * 64 + l < E.n ? E.p[j] : MFMA_TRASH;
-                P[cell] = E.v[j];
-                hc[j] = cell;
-            }
-        };
-        Ents e0, e1;
-        load_tcol(0);
+        for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
 #pragma unroll
-        for (int st = 0; st < MFMA_KS; ++st) load_b1(st);
-        load_e2(e0, 0);
-        scatter2(e0);
-        load_e2(e1, min(1, tl.w - 1));
-        load_e2(e0, min(2, tl.w - 1));
-        load_tcol(min(1, tl.w - 1));
-        auto step = [&](Ents &E, int c) {          // E holds chunk c+1; reloaded with chunk c+3
-            const int ns = (tchunk[tl.z + c].y + 3) >> 2;
-            double a[MFMA_KS];
-            const double *pa = P + (l & 15) * MFMA_PST + g;
+        for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = 0.0;
+        if (c + 1 < tl.w) scatter();
+        load_e(min(c + 2, tl.w - 1));
+        const f64x4 s0 = acc0, s1 = acc1;
 #pragma unroll
-            for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
-#pragma unroll
-            for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = 0.0;
-            if (c + 1 < tl.w) scatter2(E);
-            load_e2(E, min(c + 3, tl.w - 1));
-            bool bad = false;
-#pragma unroll
-            for (int st = 0; st < MFMA_KS; ++st) {
+        for (int st = 0; st < MFMA_KS; ++st) {
+            if (st < ns) {
                 double bb[2];
                 __builtin_memcpy(bb, &bo[st], 16);
-                bad |= st < ns && !(__builtin_isfinite(bb[0]) && __builtin_isfinite(bb[1]));
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[1], acc1, 0, 0, 0);
             }
-            if (__builtin_amdgcn_ballot_w64(bad)) {
-                sparse_chunk(c);
+            load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
+        }
+        load_tcol(min(c + 2, tl.w - 1));
+        bool bad = false;
 #pragma unroll
-                for (int st = 0; st < MFMA_KS; ++st) load_b1(st);
-            } else {
-#pragma unroll
-                for (int st = 0; st < MFMA_KS; ++st) {
-                    if (st < ns) {
-                        double bb[2];
-                        __builtin_memcpy(bb, &bo[st], 16);
-                        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[0], acc0, 0, 0, 0);
-                        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[1], acc1, 0, 0, 0);
-                    }
-                    load_b1(st);
-                }
-            }
-            load_tcol(min(c + 2, tl.w - 1));
-        };
-        for (int c = 0; c < tl.w; c += 2) {
-            step(e1, c);
-            if (c + 1 < tl.w) step(e0, c + 1);
+        for (int i = 0; i < 4; ++i) bad |= !__builtin_isfinite(acc0[i]) || !__builtin_isfinite(acc1[i]);
+        if (__builtin_amdgcn_ballot_w64(bad)) {
+            acc0 = s0, acc1 = s1;
+            sparse_chunk(c);
         }
     }
     const int c0 = 2 * (l & 15);

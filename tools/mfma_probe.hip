@@ -21,10 +21,7 @@ extern "C" int mfma_probe_launch(int ntiles, const void *tiles, const void *tchu
     auto b = (const double *)B;
     auto c = (double *)C;
     if (b_bytes >= (1ll << 32)) return -2;
-    const int v = xcd >> 1;     // kernel variant (spmm_mfma.hpp template V)
-    if (v == 1)
-        spmm_mfma_tile_kernel<true, 1><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
-    else if (xcd & 1)
+    if (xcd & 1)
         spmm_mfma_tile_kernel<true><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
     else
         spmm_mfma_tile_kernel<false><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
