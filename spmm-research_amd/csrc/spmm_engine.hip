@@ -80,9 +80,12 @@ constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.1
 constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value +0, the zero B row)
 constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
 // Matrix-core tiles (spmm_mfma_tile_kernel): fp64, 32-column panels, rows with strictly increasing
-// columns, B below 4 GiB (32-bit buffer offsets).  Policy: sampled reuse of 16-row tiles (nonzeros per union column;
-// reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE and enough tiles to fill the chip.
-constexpr double MFMA_MIN_REUSE = 2.0;
+// columns, B below 4 GiB (32-bit buffer offsets).  Policy (measured): sampled reuse of 16-row tiles
+// (nonzeros per union column; reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE, enough tiles
+// and nonzeros to fill the chip; then every 16-row tile of reuse >= MFMA_TILE_REUSE.
+constexpr double MFMA_MIN_REUSE = 3.0;      // sampled 16-row reuse of the matrix (policy)
+constexpr double MFMA_TILE_REUSE = 2.0;     // per tile, once the matrix qualifies (panel density >= 1/8)
+constexpr int64_t MFMA_MIN_NNZ = 4000000;   // smaller launches lost 0.64-0.92x (too few waves, §6.17)
 // Leftover rows of a plan whose tiles hold more than 1 - GAP_SHORT_FRAC of the nonzeros run as pieces of at most
 // GAP_SEQ_MAX nonzeros (a lone long row would otherwise be a serial straggler after the tile kernel).
 constexpr double GAP_SHORT_FRAC = 0.125;
@@ -1172,13 +1175,15 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             if (int st = load_cols()) return st;
             if (mshape && rows_strict(h->h_row_ptr.data(), hcol.data(), h->m)) {
                 const char *mthr = getenv("SPMM_HIP_MFMA_REUSE");
-                const double mreuse = (mthr && *mthr) ? atof(mthr) : (forced > 0 || fm > 0) ? 1.0 : MFMA_MIN_REUSE;
+                const bool force_m = forced > 0 || fm > 0;
+                const double mreuse = (mthr && *mthr) ? atof(mthr) : force_m ? 1.0 : MFMA_MIN_REUSE;
+                const double treuse = (mthr && *mthr) ? atof(mthr) : force_m ? 1.0 : MFMA_TILE_REUSE;
                 const double r16 = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max,
                                                      MFMA_ROWS);
-                const bool menough = (h->m + MFMA_ROWS - 1) / MFMA_ROWS >= MFMA_MIN_TILES;
-                if (forced > 0 || fm > 0 || (menough && r16 >= mreuse)) {
+                const bool menough = (h->m + MFMA_ROWS - 1) / MFMA_ROWS >= MFMA_MIN_TILES && h->nnz >= MFMA_MIN_NNZ;
+                if (force_m || (menough && r16 >= mreuse)) {
                     tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, MFMA_ROWS,
-                                        MFMA_UC, MFMA_CAPA, mreuse, tp);
+                                        MFMA_UC, MFMA_CAPA, treuse, tp);
                     if (tiles && forced <= 0 && fm <= 0 && (int64_t)tp.tiles.size() < MFMA_MIN_TILES / 2) tiles = false;
                     if (tiles && !tile_tables_fit(tp)) tiles = false;
                     if (tiles) {
