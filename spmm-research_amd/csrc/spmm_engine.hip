@@ -306,13 +306,15 @@ void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, int 
     }
 }
 
+// rs: the stream of the row kernel and the combine (the launch stream, or the handle's side stream when the row kernel
+// only runs the leftover rows of a matrix-core plan, concurrently with the tiles on s)
 template <typename T>
-void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
+void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStream_t rs) {
     T *P = (T *)h->d_part;
     for (int p = 0; p < h->plan.npanels; ++p) {
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
-        if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, s);
+        if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
         if (h->plan.ntile > 0) {
             if constexpr (std::is_same_v<T, double>) {
                 if (h->plan.tile_mfma) {
@@ -324,15 +326,26 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
         }
     }
     if (h->nlong > 0 && !h->fuse) {
-        spmm_combine_kernel<T><<<h->nlong, WG, 0, s>>>(h->d_long_rows, P, C, K);
+        spmm_combine_kernel<T><<<h->nlong, WG, 0, rs>>>(h->d_long_rows, P, C, K);
     }
 }
 
 int launch_spmm(spmm_hip_t *h, const void *B, void *C, int K, hipStream_t s) {
+    // matrix-core plans: the leftover rows (a skewed row's pieces, low-reuse tiles) run beside the tile kernel
+    const bool par = h->plan.tile_mfma && h->plan.ntile > 0 && h->nblk > 0 && h->side;
+    if (par) {
+        HIPCHK(hipEventRecord(h->ev_fork, s));
+        HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    }
+    hipStream_t rs = par ? h->side : s;
     if (h->dtype == SPMM_HIP_F64)
-        launch_spmm_t<double>(h, (const double *)B, (double *)C, K, s);
+        launch_spmm_t<double>(h, (const double *)B, (double *)C, K, s, rs);
     else
-        launch_spmm_t<float>(h, (const float *)B, (float *)C, K, s);
+        launch_spmm_t<float>(h, (const float *)B, (float *)C, K, s, rs);
+    if (par) {
+        HIPCHK(hipEventRecord(h->ev_join, h->side));
+        HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SPMM_HIP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
     return SPMM_HIP_OK;
@@ -1475,6 +1488,12 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         h->insp_bytes += tp.tiles.size() * sizeof(int4) + tp.chunks.size() * sizeof(int4) + tp.tcol.size() * 4 +
                          tp.tseg.size() * 2 + tp.tlidx.size() * 2 + tval.size();
     }
+    // the side stream of matrix-core plans (created here, never inside a run: runs may be graph-captured)
+    if (e == hipSuccess && h->plan.tile_mfma && h->nblk > 0 && !h->side) {
+        e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
         free_plan(h);
         return fail(e == hipErrorOutOfMemory ? SPMM_HIP_ERR_NOMEM : SPMM_HIP_ERR_HIP,
@@ -1852,6 +1871,12 @@ int spmm_hip_destroy(spmm_hip_t *h) {
     if (h->d_val) (void)hipFree(h->d_val);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    if (h->side) {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+    }
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SPMM_HIP_OK;

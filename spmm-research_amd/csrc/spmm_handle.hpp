@@ -122,6 +122,8 @@ struct spmm_hip_handle {
 
     const void *last_x = nullptr;
     hipStream_t stream = nullptr;  // own stream for spmm_hip_run
+    hipStream_t side = nullptr;    // matrix-core plans: the row kernel's leftover rows run here, beside the tiles
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev[8] = {};
     bool have_times = false, have_transpose = false, have_copies = false;
     bool rec_events = false;         // run_device records timing events (spmm_hip_set_timing / SPMM_HIP_EVENTS=1)
