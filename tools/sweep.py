@@ -59,6 +59,14 @@ def dataset_index_lines(args) -> list[tuple[int, str]]:
         idx.sort(key=lambda i: (bitrev4[i % 16], i))
     if args.sort_by_size:
         idx.sort(key=lambda i: int(lines[i].split()[0]) * float(lines[i].split()[2]))
+    if getattr(args, "where", ""):
+        # generator-parameter filter, e.g. "crs=0.95,min_avg=20" (field 10 = cross-row similarity, 3 = avg nnz/row)
+        cond = dict(kv.split("=") for kv in args.where.split(","))
+        def keep(l):
+            g = l.split()
+            return (("crs" not in cond or float(g[9]) == float(cond["crs"])) and
+                    ("min_avg" not in cond or float(g[2]) >= float(cond["min_avg"])))
+        idx = [i for i in idx if keep(lines[i])]
     return [(i, lines[i]) for i in idx[args.offset::args.stride]]
 
 
@@ -169,6 +177,7 @@ def main():
     ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--offset", type=int, default=0)
     ap.add_argument("--sort-by-size", action="store_true")
+    ap.add_argument("--where", default="", help="generator-parameter filter, e.g. crs=0.95,min_avg=20")
     ap.add_argument("--order", choices=["dataset", "interleave16"], default="dataset",
                     help="interleave16: every 16th line first, then offsets 8, 4, 12, 2, ... (even class coverage)")
     ap.add_argument("--k", default="32")
@@ -323,7 +332,7 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
                    "engine_sha256": sha, "batches": [round(x, 5) for x in ms_b], "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
                    "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
                    "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
-                   "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
+                   "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]), "tile_mode": mf.tile_info()["mode"],
                    "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
                               "timed": round(t_timed, 3), "check": round(t_check, 3)},
                    **par}

@@ -7,10 +7,10 @@
 # gpurun_out/sweep/<name>.<stamp>[.w<i>].jsonl, and the call stops starting matrices after <budget_s>.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-BUDGET=${1:-1000}; NAME=${2:-r03_sweep_medium}; KS=${3:-1,8,32,128}; WORKERS=${4:-1}
+BUDGET=${1:-1000}; NAME=${2:-r03_sweep_medium}; KS=${3:-1,8,32,128}; WORKERS=${4:-1}; WHERE=${5:-}
 OUT=gpurun_out/sweep
 mkdir -p $OUT
 STAMP=$(date +%s)
 timeout -k 10 $((BUDGET + 170)) python -u tools/sweep.py --order interleave16 --k $KS --budget $BUDGET \
-    --workers $WORKERS --done profiles/$NAME.done --out $OUT/$NAME.$STAMP.jsonl > $OUT/$NAME.$STAMP.log 2>&1
+    --workers $WORKERS --done profiles/$NAME.done ${WHERE:+--where $WHERE} --out $OUT/$NAME.$STAMP.jsonl > $OUT/$NAME.$STAMP.log 2>&1
 rc=$?; tail -n 2 $OUT/$NAME.$STAMP.log | cut -c1-200; cat $OUT/$NAME.$STAMP*.jsonl | wc -l; exit $rc
