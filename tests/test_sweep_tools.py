@@ -42,3 +42,19 @@ def test_sample_parity_checks_exact_and_inexact_rows():
     Ct[1] += 1e-300 if Ct[1, 0] == 0 else Ct[1, 0] * 1e-15   # an exact row one ulp-ish off
     r = sweep.sample_parity(S, O, A, B, Ct, k, 3000, np.random.default_rng(0), np.float64, exact)
     assert not r["bitexact_seq_rows"]
+
+
+def test_sweep_where_filter_selects_the_matrix_core_classes():
+    """tools/sweep.py --where (the final-build re-sweep of DESIGN §6.17): crs 0.95 and >= 20 nonzeros per row is one
+    third of the cross-row-similarity grid times four of the six row-length classes, in interleave16 order."""
+    import argparse
+    import sweep
+    a = argparse.Namespace(line=None, dataset="medium", order="interleave16", sort_by_size=False, offset=0, stride=1,
+                           where="crs=0.95,min_avg=20")
+    sel = sweep.dataset_index_lines(a)
+    assert len(sel) == 3596
+    assert all(float(l.split()[9]) == 0.95 and float(l.split()[2]) >= 20 for _, l in sel)
+    a.where = ""
+    full = sweep.dataset_index_lines(a)
+    assert len(full) == 16190
+    assert [i for i, _ in sel] == [i for i, l in full if float(l.split()[9]) == 0.95 and float(l.split()[2]) >= 20]
