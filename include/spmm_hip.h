@@ -251,6 +251,22 @@ int spmm_hip_debug_tiles(const int32_t *row_ptr, const int32_t *col_idx, int64_t
 void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t);
 
 
+/* Diagnostics (host only): the inspector's decisions for (CSR, k, dtype) without a device -- what spmm_hip_plan would
+ * plan (tools/plan_census.py runs it over the whole medium dataset).  mfma: the SPMM_HIP_MFMA override (-1 no
+ * matrix-core tiles, 0 policy, 1 every eligible tile, 2 the policy's gate forced open).  gate_only != 0: stop after
+ * the matrix-core gate, which reads the columns of its sampled 16-row tiles only (rows t*16 .. t*16+15 for
+ * t = i * ceil(m/16) / min(256, ceil(m/16)), i = 0..); col_idx then only needs those rows filled.  out has
+ * SPMM_HIP_PLAN_SLOTS doubles: [0] tile mode (0 none, 1 LDS, 2 matrix-core; gate-only: 2 or 0), [1] gate verdict,
+ * [2] sampled 16-row reuse, [3] fraction of sampled tiles taken, [4] est. nonzeros in taken tiles, [5] est. chunks,
+ * [6] largest sampled chunk count, [7] model time with tiles (us), [8] model time without (us), [9] tiles sampled,
+ * [10] split length T, [11] piece length of rows > T, [12] K-panel width, [13] K panels, [14] tiles built,
+ * [15] nonzeros in tiles, [16] chunks, [17] row-kernel blocks, [18] split rows, [19] exact rows, [20] vector lanes,
+ * [21] XCD order, [22] column windows, [23] 1 = gate only, [24]/[25] plan fingerprint (low / high 32 bits; two
+ * plans are the same exactly when these agree). */
+#define SPMM_HIP_PLAN_SLOTS 32
+int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t k,
+                        int32_t dtype, int32_t mfma, int32_t gate_only, double *out);
+
 const char *spmm_hip_strerror(int status);
 const char *spmm_hip_last_error_detail(void);
 int spmm_hip_device_count(int *count);

@@ -84,6 +84,10 @@ int spmm_host_generate_row_ptr(const spmm_gen_params_t *p, int32_t *row_ptr /* [
 
 /* Rows [r0, r1) of the same matrix: out->row_ptr is rebased to start at 0; column ids stay global. */
 int spmm_host_generate_rows(const spmm_gen_params_t *p, int64_t r0, int64_t r1, spmm_csr_t *out);
+/* The whole matrix's row_ptr, with the columns and values of the rows where mask[i] != 0 only (the other rows'
+ * entries are zero); the masked rows equal those of spmm_host_generate.  Only the generator segments holding a
+ * masked row are generated (a row sample of a large matrix: tools/plan_census.py). */
+int spmm_host_generate_masked(const spmm_gen_params_t *p, const uint8_t *mask, spmm_csr_t *out);
 
 int spmm_host_features(const spmm_csr_t *a, spmm_features_t *f);
 

@@ -77,15 +77,13 @@ constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgr
                                           // (measured, DESIGN §6.9: 1.22x at ~14 on 39 K x 500 bw 0.05; 0.66-0.82x
                                           // at 4.5-6; the kernel is LDS-throughput bound)
 constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
-constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value +0, the zero B row)
+constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value -0, the zero B row)
 constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
 // Matrix-core tiles (spmm_mfma_tile_kernel): fp64, 32-column panels, rows with strictly increasing
 // columns, B below 4 GiB (32-bit buffer offsets).  Policy (measured): sampled reuse of 16-row tiles
 // (nonzeros per union column; reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE, enough tiles
 // and nonzeros to fill the chip; then every 16-row tile of reuse >= MFMA_TILE_REUSE.
-constexpr double MFMA_MIN_REUSE = 3.0;      // sampled 16-row reuse of the matrix (policy)
 constexpr double MFMA_TILE_REUSE = 2.0;     // per tile, once the matrix qualifies (panel density >= 1/8)
-constexpr int64_t MFMA_MIN_NNZ = 4000000;   // smaller launches lost 0.64-0.92x (too few waves, §6.17)
 // Leftover rows of a plan whose tiles hold more than 1 - GAP_SHORT_FRAC of the nonzeros run as pieces of at most
 // GAP_SEQ_MAX nonzeros (a lone long row would otherwise be a serial straggler after the tile kernel).
 constexpr double GAP_SHORT_FRAC = 0.125;
@@ -289,20 +287,25 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
     }
 }
 
-// Matrix-core tiles for a 32-column fp64 panel: four 16-row tiles (one per wave) per workgroup.
-// B and C point at the panel's first column; the buffer descriptor of B covers the rest of the array.
+// Matrix-core tiles over columns [k0, k0 + kw) (kw a multiple of 32): four 16-row tiles (one per wave) per
+// workgroup; a wave owns 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (DESIGN §6.18;
+// SPMM_HIP_MFMA_NP=1 keeps 32).  B and C point at column k0; the buffer descriptor of B covers the rest of the array.
 void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, int kw, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
-    for (int k1 = 0; k1 + 32 <= kw; k1 += 32) {            // the kernel covers 32 columns: sub-panels of this panel
+    const int np_max = env_int("SPMM_HIP_MFMA_NP", 2) >= 2 ? 2 : 1;
+    for (int k1 = 0; k1 + 32 <= kw;) {
+        const int np = (np_max >= 2 && k1 + 64 <= kw) ? 2 : 1;
         const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)(k0 + k1)) * sizeof(double));
-        if (h->plan.tile_xcd)
-            spmm_mfma_tile_kernel<true><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
-                                                            (const double *)h->d_tval, h->d_tlidx, B + k1, bb,
-                                                            C + k1, ld);
-        else
-            spmm_mfma_tile_kernel<false><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol,
-                                                             (const double *)h->d_tval, h->d_tlidx, B + k1, bb,
-                                                             C + k1, ld);
+        auto go = [&](auto xcd_c, auto np_c) {
+            spmm_mfma_tile_kernel<decltype(xcd_c)::value, decltype(np_c)::value><<<grid, WG, 0, s>>>(
+                h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const double *)h->d_tval, h->d_tlidx, B + k1, bb,
+                C + k1, ld);
+        };
+        using N1 = std::integral_constant<int, 1>;
+        using N2 = std::integral_constant<int, 2>;
+        if (h->plan.tile_xcd) np == 2 ? go(std::true_type(), N2()) : go(std::true_type(), N1());
+        else np == 2 ? go(std::false_type(), N2()) : go(std::false_type(), N1());
+        k1 += 32 * np;
     }
 }
 
@@ -311,19 +314,15 @@ void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, int 
 template <typename T>
 void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStream_t rs) {
     T *P = (T *)h->d_part;
+    // matrix-core tiles: one pass over all K columns (the row kernel's K panels are for its B gather, not theirs)
+    if constexpr (std::is_same_v<T, double>) {
+        if (h->plan.ntile > 0 && h->plan.tile_mfma) launch_mfma(h, B, C, K, 0, K, s);
+    }
     for (int p = 0; p < h->plan.npanels; ++p) {
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
         if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
-        if (h->plan.ntile > 0) {
-            if constexpr (std::is_same_v<T, double>) {
-                if (h->plan.tile_mfma) {
-                    launch_mfma(h, B + k0, C + k0, K, k0, kw, s);
-                    continue;
-                }
-            }
-            launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
-        }
+        if (h->plan.ntile > 0 && !h->plan.tile_mfma) launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
     }
     if (h->nlong > 0 && !h->fuse) {
         spmm_combine_kernel<T><<<h->nlong, WG, 0, rs>>>(h->d_long_rows, P, C, K);
@@ -453,8 +452,10 @@ void pack_blocks(const std::vector<int32_t> &vp, int64_t v0, int64_t v1, int cap
 // Virtual rows (rows longer than T cut into T-nonzero pieces) packed into blocks (one column window).
 // skip (optional): rows computed elsewhere (tiles).  A run of skipped rows becomes one GAP virtual row (destination
 // 0, never in a block) so the virtual-row offsets stay one prefix array; blocks never cross a gap.
+// piece: length of the pieces rows longer than T are cut into (0 = T).
 void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool heavy_first = true,
-             const uint8_t *skip = nullptr, int max_rows = CAP_ROWS) {
+             const uint8_t *skip = nullptr, int max_rows = CAP_ROWS, int piece = 0) {
+    const int P = piece > 0 ? piece : T;
     out = Inspection();
     out.vrow_ptr.reserve((size_t)m + 1);
     out.vrow_ptr.push_back(rp[0]);
@@ -476,10 +477,10 @@ void inspect(const int32_t *rp, int64_t m, int T, int cap, Inspection &out, bool
             out.vdest.push_back((int32_t)r);
         } else {
             any_split = true;
-            const int pieces = (int)((len + T - 1) / T);
+            const int pieces = (int)((len + P - 1) / P);
             out.long_rows.push_back(make_int4((int)r, out.nslots, pieces, 0));
             for (int q = 0; q < pieces; ++q) {
-                out.vrow_ptr.push_back((int32_t)std::min<int64_t>((int64_t)rp[r] + (int64_t)(q + 1) * T, rp[r + 1]));
+                out.vrow_ptr.push_back((int32_t)std::min<int64_t>((int64_t)rp[r] + (int64_t)(q + 1) * P, rp[r + 1]));
                 out.vdest.push_back(-(out.nslots + q) - 1);
             }
             out.nslots += pieces;
@@ -958,6 +959,414 @@ double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64
     return n > 0 ? sum / (double)n : 0.0;
 }
 
+// ------------------------------------------------------------------------------------ matrix-core policy (gate)
+// Whether a matrix runs its dense 16-row tiles on the matrix cores.  Decided from a sample of
+// MFMA_GATE_SAMPLE evenly spaced 16-row candidate tiles -- the gate reads the columns of those rows only (so a
+// census of the whole medium dataset can evaluate it from the sampled rows, tools/plan_census.py) -- plus m, nnz and
+// the panel shape: per sampled tile its nonzeros, union columns and the chunks build_tiles would cut; the taken ones
+// (reuse >= MFMA_TILE_REUSE) scaled to the matrix give the work of the tile kernel and of the row kernel on the same
+// rows, priced by mfma_cost (measured constants).
+constexpr int MFMA_GATE_SAMPLE = 256;
+struct MfmaGate {
+    int sampled = 0;          // candidate tiles sampled (all rows <= T, not empty)
+    double r16 = 0.0;         // mean reuse of the sampled tiles (nonzeros per union column)
+    double take = 0.0;        // fraction of sampled tiles the build would take (reuse >= MFMA_TILE_REUSE)
+    double tile_nnz = 0.0;    // estimated nonzeros in taken tiles (whole matrix)
+    double chunks = 0.0;      // estimated chunks of the taken tiles (whole matrix)
+    double max_chunks = 0.0;  // largest chunk count of a sampled taken tile
+    double t_on = 0.0, t_off = 0.0;   // cost model (us): tiles + leftover rows vs the row kernel alone
+    int verdict = 0;          // 1 = matrix-core tiles
+};
+
+MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T) {
+    MfmaGate g;
+    if (m == 0) return g;
+    std::vector<int32_t> stamp((size_t)ncols, -1);
+    const int64_t ntiles = (m + MFMA_ROWS - 1) / MFMA_ROWS;
+    const int64_t ns = std::min<int64_t>(MFMA_GATE_SAMPLE, ntiles);
+    const int64_t room = MFMA_CAPA - (int64_t)MFMA_ROWS * (TILE_SEG_ALIGN - 1);
+    double sum_r = 0.0, nz_taken = 0.0, ch_taken = 0.0, n_taken = 0.0;
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t t = i * ntiles / ns;
+        const int64_t r0 = t * MFMA_ROWS, r1 = std::min<int64_t>(m, r0 + MFMA_ROWS);
+        bool ok = true;
+        for (int64_t r = r0; r < r1 && ok; ++r) ok = (int64_t)rp[r + 1] - rp[r] <= T;
+        if (!ok || rp[r1] == rp[r0]) continue;
+        int64_t nu = 0;
+        const double reuse = tile_reuse(rp, col, r0, r1, stamp, (int32_t)i, 0.0, &nu);
+        sum_r += reuse;
+        ++g.sampled;
+        if (reuse >= MFMA_TILE_REUSE) {
+            const double nnz = (double)(rp[r1] - rp[r0]);
+            const double ch = std::max(std::ceil((double)nu / MFMA_UC), std::ceil(nnz / (double)room));
+            nz_taken += nnz, ch_taken += ch, n_taken += 1.0;
+            g.max_chunks = std::max(g.max_chunks, ch);
+        }
+    }
+    if (g.sampled == 0) return g;
+    g.r16 = sum_r / g.sampled;
+    g.take = n_taken / g.sampled;
+    const double scale = (double)ntiles / (double)ns;   // sampled slots -> all candidate slots
+    g.tile_nnz = nz_taken * scale;
+    g.chunks = ch_taken * scale;
+    return g;
+}
+
+// The gate.  Cost model (us per K panel of 32 columns), fitted on same-process A/B data (tools/mfma_ab.py,
+// profiles/r04/ab/):
+//   row kernel:   t_row(nnz, rows) = launch + nnz / R_ROW(reuse)     (a 256-B B row gathered per nonzero; dense
+//                 rows hit L2, so the rate grows with the tile reuse)
+//   tile kernel:  t_mfma = launch + max(chunks / (CHUNK_RATE * waves_in_flight), max_chunks * CHUNK_LAT)
+// Matrix-core tiles are taken when t_on = max(t_mfma, t_row(leftover)) beats t_off = t_row(all) by MFMA_MIN_GAIN.
+constexpr double MFMA_MIN_REUSE = 3.0;      // sampled 16-row reuse of the matrix (policy)
+constexpr int64_t MFMA_MIN_NNZ = 4000000;   // smaller launches lost 0.64-0.92x (too few waves, §6.17)
+void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k) {
+    (void)k;
+    g.verdict = ((m + MFMA_ROWS - 1) / MFMA_ROWS >= MFMA_MIN_TILES && nnz >= MFMA_MIN_NNZ && g.r16 >= MFMA_MIN_REUSE)
+                    ? 1 : 0;
+}
+
+// Everything the inspector decides for (matrix, K), on the host: the plan, the tile plan, the block decomposition,
+// the exact-row mask and the fused-combine slot table.  spmm_hip_plan turns it into device tables;
+// spmm_hip_debug_plan reports it without a device.
+struct Draft {
+    Plan pl;
+    TilePlan tp;
+    bool tiles = false;
+    Inspection in;
+    int64_t W = 0;
+    std::vector<int32_t> slot_lr;
+    bool fuse = false;
+    std::vector<uint8_t> exact;
+    MfmaGate gate;
+    bool gate_only = false;      // stopped after the matrix-core gate (census mode, no full tile build)
+};
+
+// hcol_in: the matrix's columns on the host (nullptr: read from the handle's device copy).  gate_only: stop after
+// the matrix-core gate, which reads only its sampled rows' columns (tools/plan_census.py passes a column array
+// filled for those rows only).
+int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_only, Draft &d) {
+    Plan &pl = d.pl;
+    pl = Plan();
+    pl.k = k;
+    // K panels of PANEL_ROW_BYTES-byte B rows when B would crowd the Infinity Cache and the B gather dominates the
+    // launch (>= 16 nonzeros per row); each extra panel re-streams A and cuts C rows into 256-B pieces, which only
+    // pays when it turns Infinity-Cache misses into hits (measured §6.2: config 2 K=128 1.65 ms at 32 columns vs
+    // 2.30 ms unpanelled; a 200 K-row, 10 nnz/row matrix with a 208 MB B is faster unpanelled).
+    const int panel_env = env_int("SPMM_HIP_PANEL_K", 0);
+    const double b_bytes = (double)h->ncols * k * (double)h->vsize;
+    const double avg_row = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    pl.kw = k;
+    if (h->var.panel_k > 0 || panel_env > 0) {
+        pl.kw = std::min(k, h->var.panel_k > 0 ? h->var.panel_k : panel_env);
+    } else if (b_bytes > PANEL_MIN_B_BYTES && avg_row >= PANEL_MIN_ROW_NNZ) {
+        pl.kw = std::min(k, std::max(1, (int)(PANEL_ROW_BYTES / h->vsize)));
+    }
+    // col_idx on the host (span, row similarity, windows, XCD order) when some policy below may need it
+    std::vector<int32_t> hstore;
+    const int32_t *hcol = nullptr;
+    double span = (double)h->ncols, crs = 1.0;
+    auto load_cols = [&]() -> int {
+        if (hcol || h->nnz == 0) return SPMM_HIP_OK;
+        if (hcol_in) {
+            hcol = hcol_in;
+        } else {
+            hstore.resize((size_t)h->nnz);
+            HIPCHK(hipMemcpy(hstore.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
+            hcol = hstore.data();
+        }
+        if (!gate_only) {
+            span = mean_row_span(h->h_row_ptr.data(), hcol, h->m);
+            crs = row_similarity_sample(h->h_row_ptr.data(), hcol, h->m);
+        }
+        return SPMM_HIP_OK;
+    };
+    if (!gate_only && h->var.panel_k <= 0 && panel_env <= 0 && (double)pl.kw * h->vsize == 2.0 * WIN_LINE &&
+        avg_row >= NARROW_MIN_ROW && h->m > 1) {
+        if (int st = load_cols()) return st;
+        const double x = span * 2.0 * WIN_LINE / WIN_L2_BYTES;
+        if (crs < NARROW_MAX_CRS && x >= NARROW_MIN_SPAN_L2 && x <= NARROW_MAX_SPAN_L2) pl.kw /= 2;
+    }
+    pl.npanels = (k + pl.kw - 1) / pl.kw;
+    // block capacity and split length
+    int vec, g;
+    lane_layout(pl.kw, k, h->vsize, vec, g);
+    // block capacity: the LDS window (CAP), smaller for small matrices so >= ~1024 blocks exist (a 4096-nonzero
+    // window for one-lane row groups measured slower at K = 1, §6.2)
+    const int cap_env = env_int("SPMM_HIP_CAP", 0);
+    pl.cap = h->var.cap > 0 ? std::min(h->var.cap, CAP)
+             : cap_env > 0   ? std::min(cap_env, CAP)
+                             : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
+    const int seq_env = env_int("SPMM_HIP_SEQ_MAX", 0);
+    pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max : seq_env > 0 ? seq_env : split_length(h, pl.kw);
+    pl.seq_max = std::max(1, std::min(pl.seq_max, CAP));
+    pl.cap = std::max(pl.cap, std::min(CAP, pow2_ceil(pl.seq_max)));   // a row of T nonzeros fits one block
+    pl.piece = pl.seq_max;
+    // rows per block: one row per row group when a group's row is long (>= 64 nonzeros) and a block of NG rows fits
+    // the LDS window -- the greedy packing would otherwise put NG + a few rows in a block and make a quarter of the
+    // groups run two rows while the rest idle (measured K=32, avg 100: 1.03-1.13x; avg 500 blocks hold < NG rows
+    // anyway; avg 20-50 unchanged or slower, r03_s2 / r03_s3 probes, DESIGN §6.13)
+    {
+        int vec_b, g_b;
+        lane_layout(pl.kw, k, h->vsize, vec_b, g_b);
+        const int ng = WG / g_b;
+        const int env_rows = env_int("SPMM_HIP_BLOCK_ROWS", 0);
+        pl.block_rows = CAP_ROWS;
+        if (env_rows > 0)
+            pl.block_rows = std::min(CAP_ROWS, env_rows);
+        else if (avg_row >= 64.0 && (double)ng * avg_row <= (double)pl.cap)
+            pl.block_rows = ng;
+    }
+
+    const int64_t srow_t = (int64_t)pl.kw * (int64_t)h->vsize;
+    // LDS B tiles (DESIGN §3.4): rows whose union of columns is reused enough leave the row kernel.  Needs 16-byte
+    // B pieces in every panel and sorted rows.  SPMM_HIP_TILES=-1 off / 1 every eligible tile; SPMM_HIP_TILE_REUSE
+    // sets the policy threshold.
+    TilePlan &tp = d.tp;
+    bool &tiles = d.tiles;
+    tiles = false;
+    {
+        const int64_t srow = srow_t;
+        const int env_t = env_int("SPMM_HIP_TILES", 0);
+        const int forced = h->var.tiles != 0 ? h->var.tiles : env_t;
+        int vec_t, g_t;
+        lane_layout(pl.kw, k, h->vsize, vec_t, g_t);
+        const bool shape_ok = h->nnz > 0 && vec_t == (int)(16 / h->vsize) && ((int64_t)k * h->vsize) % 16 == 0 &&
+                              srow % 16 == 0 && k % pl.kw == 0 && srow >= 64 && srow <= 1024 &&
+                              pow2_ceil(srow / 16) == srow / 16 &&
+                              h->ncols < INT32_MAX;
+        const int64_t win_forced = h->var.win_bytes != 0 ? h->var.win_bytes : (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
+        // matrix-core tiles first: fp64 32-column panels, strictly increasing columns, B < 4 GiB.
+        // SPMM_HIP_MFMA: -1 off, 0 policy (the gate), 1 every eligible tile of reuse >= 1, 2 the gate open with the
+        // policy's per-tile threshold (what the policy runs once a matrix qualifies; A/B measurements)
+        const int env_m = env_int("SPMM_HIP_MFMA", 0);
+        const int fm = h->var.mfma != 0 ? h->var.mfma : env_m;
+        const bool mshape = fm >= 0 && h->vsize == 8 && k % 32 == 0 &&
+                            (double)h->ncols * (double)k * 8.0 < 4294967296.0;
+        if (forced >= 0 && h->nnz > 0 && h->ncols < INT32_MAX && win_forced <= 0 && (mshape || shape_ok)) {
+            if (int st = load_cols()) return st;
+            if (mshape && (gate_only || rows_strict(h->h_row_ptr.data(), hcol, h->m))) {
+                const char *mthr = getenv("SPMM_HIP_MFMA_REUSE");
+                const bool force_all = forced > 0 || fm == 1;
+                const double treuse = (mthr && *mthr) ? atof(mthr) : force_all ? 1.0 : MFMA_TILE_REUSE;
+                d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max);
+                mfma_cost(d.gate, h->m, h->nnz, k);
+                if (mthr && *mthr && fm <= 0) d.gate.verdict = d.gate.r16 >= atof(mthr) ? 1 : 0;
+                pl.tile_reuse = d.gate.r16;
+                if (gate_only) {
+                    d.gate_only = true;
+                    pl.tile_mfma = (force_all || fm == 2 || d.gate.verdict) ? 1 : 0;
+                    return SPMM_HIP_OK;
+                }
+                if (force_all || fm == 2 || d.gate.verdict) {
+                    tiles = build_tiles(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, MFMA_ROWS,
+                                        MFMA_UC, MFMA_CAPA, treuse, tp);
+                    if (tiles && !force_all && fm != 2 && (int64_t)tp.tiles.size() < MFMA_MIN_TILES / 2) tiles = false;
+                    if (tiles && !tile_tables_fit(tp)) tiles = false;
+                    if (tiles) pl.tile_mfma = 1;
+                }
+            }
+            if (gate_only) {        // census mode: the matrix-core gate is all it reports
+                d.gate_only = true;
+                return SPMM_HIP_OK;
+            }
+            if (!tiles && shape_ok && rows_sorted(h->h_row_ptr.data(), hcol, h->m)) {
+                const int rows_env = env_int("SPMM_HIP_TILE_ROWS", 0);
+                int rmax = std::min((WG / g_t) * tile_rpg(g_t), rows_env > 0 ? rows_env : TILE_ROWS);
+                const char *thr = getenv("SPMM_HIP_TILE_REUSE");
+                const double min_reuse = forced > 0 ? 1.0 : (thr && *thr) ? atof(thr) : TILE_MIN_REUSE;
+                pl.tile_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, rmax);
+                const bool enough = (h->m + rmax - 1) / rmax >= TILE_MIN_TILES && srow <= TILE_POLICY_MAX_ROW;
+                if (forced > 0 || (enough && pl.tile_reuse >= min_reuse))
+                    tiles = build_tiles(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, rmax,
+                                        (int)(TILE_UCB / srow), TILE_CAPA, min_reuse, tp,
+                                        tile_colmax_for(h->vsize, g_t) - 4, TILE_DMAX - 1);
+                if (tiles && forced <= 0 && (int64_t)tp.tiles.size() < TILE_MIN_BUILT) tiles = false;
+                if (tiles && !tile_tables_fit(tp)) tiles = false;     // 32-bit tile positions (row kernel instead)
+            }
+        }
+        if (gate_only) {
+            d.gate_only = true;
+            return SPMM_HIP_OK;
+        }
+        if (tiles) {
+            pl.ntile = (int)tp.tiles.size();
+            pl.tile_rows = tp.rows;
+            pl.tile_nnz = tp.nnz;
+            pl.tile_chunks = (int64_t)tp.chunks.size() - 1;
+            // consecutive tiles share most of their columns: in XCD order they share an L2 as well
+            const int env_x = env_int("SPMM_HIP_TILE_XCD", 1);
+            pl.tile_xcd = (env_x > 0 && pl.ntile >= 64) ? 1 : 0;
+            // compute-lane width in 16-byte pieces: the requested 1/2/4, lowered until rows per group divide
+            int sw = std::max(1, env_int("SPMM_HIP_TILE_WIDE", TILE_WIDE_DEFAULT));
+            sw = sw >= 2 ? 2 : 1;
+            while (sw > 1 && tile_rpg(g_t) % sw != 0) sw /= 2;
+            pl.tile_wide = sw;
+        } else {
+            pl.tile_mfma = 0;
+        }
+    }
+
+    // XCD-contiguous order, else column windows (chained mode; needs every row's columns sorted); both decided from
+    // col_idx on the host
+    Inspection &in = d.in;
+    int64_t &W = d.W;
+    W = 0;
+    {
+        const double srow = (double)pl.kw * (double)h->vsize;
+        const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
+        const int64_t forced = h->var.win_bytes != 0 ? h->var.win_bytes : env_bytes;
+        const bool b_big = (double)h->ncols * std::max(srow, WIN_LINE) > WIN_MIN_SPAN_NARROW * WIN_L2_BYTES;
+        const bool maybe_win = h->nnz > 0 && forced >= 0 && (forced > 0 || (b_big && (srow >= WIN_MIN_ROW_BYTES || srow <= WIN_TINY_ROW_BYTES)));
+        const bool maybe_xcd = h->nnz > 0 && (double)h->ncols * srow > WIN_L2_BYTES;
+        if (maybe_win || maybe_xcd) {
+            if (int st = load_cols()) return st;
+        }
+        pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
+        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) &&
+            rows_sorted(h->h_row_ptr.data(), hcol, h->m)) {
+            std::vector<Piece> pcs;
+            Inspection tmp;
+            make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
+            W = window_cols(h, pl.kw, pcs, hcol, h->var.win_bytes, crs, &pl.nseg);
+        }
+    }
+    if (W > 0) {
+        pl.xcd = 0;
+        inspect_windows(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, pl.cap, W, in, pl.block_rows);
+        pl.win_cols = W;
+        pl.nwin = (int)in.win_blk.size() - 1;
+        pl.nseg = (int64_t)in.vdest.size();
+    } else {
+        // when tiles hold nearly all the work, the row kernel's launch is only the leftover rows -- typically one
+        // skewed row of thousands of nonzeros whose T-pieces each run as a latency-bound serial chain (~64 us for
+        // 2,048 gathers) after the tile kernel: the rows longer than T are cut into GAP_SEQ_MAX-nonzero pieces
+        // instead (rows of <= T nonzeros stay whole, one exact chain)
+        if (tiles && pl.tile_mfma && (double)(h->nnz - tp.nnz) < GAP_SHORT_FRAC * (double)h->nnz &&
+            pl.seq_max > GAP_SEQ_MAX && h->var.seq_max <= 0 && env_int("SPMM_HIP_SEQ_MAX", 0) <= 0)
+            pl.piece = GAP_SEQ_MAX;
+        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd,
+                tiles ? tp.in_tile.data() : nullptr, pl.block_rows, pl.piece);
+        pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
+    }
+    const int nblk = (int)in.blk.size();
+    // vector lanes when the staged blocks hold fewer rows than row groups (long rows at small K; DESIGN §6.4), and
+    // the exact-row mask: rows <= T whose every virtual row sits in a block with L = 1
+    {
+        int vec, g;
+        lane_layout(pl.kw, k, h->vsize, vec, g);
+        const int ng = WG / g;
+        const int lcap = std::max(1, 64 / g);
+        // the rows the row kernel runs: gap virtual rows and the tile rows' nonzeros are not among them
+        const double nvr = (double)((int64_t)in.vrow_ptr.size() - 1 - in.ngaps);
+        const double nnz_rows = (double)(h->nnz - (tiles ? tp.nnz : 0));
+        const double rows_per_block = in.blk.empty() ? 0.0 : nvr / (double)nblk;
+        const double mean_vrow = nvr > 0 ? nnz_rows / nvr : 0.0;
+        const int env_l = env_int("SPMM_HIP_LANES", 0);
+        const int forced = h->var.lanes != 0 ? h->var.lanes : env_l;
+        bool all_blocks = false;
+        if (forced != 0)
+            all_blocks = forced > 0, pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
+        else
+            all_blocks = nnz_rows > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW,
+            pl.lmax = all_blocks ? lcap : 1;
+        // flag the blocks that may use vector lanes: all of them under the policy, else (unless disabled) the blocks
+        // made only of split-row pieces (inexact anyway; a 16 M-nonzero row is thousands of one-piece blocks)
+        auto dest_of = [&](int v) -> int64_t {
+            if (in.vdest.empty()) return v;
+            return (W > 0) ? (in.vdest[v] >> 1) : in.vdest[v];
+        };
+        bool any_flag = false;
+        for (int2 &bk : in.blk) {
+            bool ok = all_blocks;
+            if (!ok && forced >= 0 && !in.long_rows.empty() && bk.y - bk.x < ng) {
+                ok = true;
+                for (int v = bk.x; v < bk.y && ok; ++v) ok = dest_of(v) < 0;
+            }
+            if (ok) bk.y |= BLK_VL_FLAG, any_flag = true;
+        }
+        if (any_flag && pl.lmax <= 1) pl.lmax = lcap;
+        d.exact.assign((size_t)h->m, 1);
+        for (const int4 &lr : in.long_rows) d.exact[(size_t)lr.x] = 0;
+        if (pl.lmax > 1) {
+            for (const int2 &bk : in.blk) {
+                if (!(bk.y & BLK_VL_FLAG)) continue;
+                const int e = bk.y & BLK_ROWS_MASK, nrows = e - bk.x;
+                if (nrows >= ng) continue;
+                int L = 1;
+                while (2 * L <= ng / nrows) L *= 2;
+                if (std::min(L, pl.lmax) <= 1) continue;
+                for (int v = bk.x; v < e; ++v) {
+                    const int64_t dd = dest_of(v);
+                    if (dd >= 0) d.exact[(size_t)dd] = 0;
+                }
+            }
+        }
+        pl.exact_rows = 0;
+        for (uint8_t e : d.exact) pl.exact_rows += e;
+    }
+    // fused combine (DESIGN §3.2): split rows summed by the block that stores their last piece, so no combine
+    // launch.  Needs one launch per panel (no column windows), partials below 4 GiB (32-bit buffer offsets) and each
+    // split row's pieces in consecutive virtual rows with consecutive slots (what inspect() builds; checked here).
+    // SPMM_HIP_FUSE=0 keeps the separate spmm_combine_kernel.
+    {
+        std::vector<int32_t> &slot_lr = d.slot_lr;
+        const int nslots = in.nslots;
+        bool fuse = nslots > 0 && W == 0 && env_int("SPMM_HIP_FUSE", 1) != 0 &&
+                    (uint64_t)nslots * (uint64_t)k * h->vsize < (1ULL << 32);
+        if (fuse) {
+            slot_lr.assign((size_t)nslots, -1);
+            std::vector<int64_t> slot_v((size_t)nslots, -1);
+            for (size_t v = 0; v < in.vdest.size(); ++v)
+                if (in.vdest[v] < 0) slot_v[(size_t)(-in.vdest[v] - 1)] = (int64_t)v;
+            for (size_t li = 0; li < in.long_rows.size() && fuse; ++li) {
+                const int4 lr = in.long_rows[li];
+                for (int q = 0; q < lr.z && fuse; ++q) {
+                    const int sl = lr.y + q;
+                    fuse = sl < nslots && slot_v[(size_t)sl] >= 0 && slot_lr[(size_t)sl] < 0 &&
+                           (q == 0 || slot_v[(size_t)sl] == slot_v[(size_t)sl - 1] + 1);
+                    if (fuse) slot_lr[(size_t)sl] = (int32_t)li;
+                }
+            }
+            for (int32_t x : slot_lr) fuse = fuse && x >= 0;
+        }
+        if (fuse) {
+            for (int2 &bk : in.blk) {
+                const int e = bk.y & BLK_ROWS_MASK;
+                for (int v = bk.x; v < e; ++v)
+                    if (in.vdest[(size_t)v] < 0) {
+                        bk.y |= BLK_SPLIT_FLAG;
+                        break;
+                    }
+            }
+        }
+        d.fuse = fuse;
+        if (!fuse) slot_lr.clear();
+    }
+    return SPMM_HIP_OK;
+}
+
+// FNV-1a over the plan's decisions and tables (spmm_hip_debug_plan: two builds or two policies plan a matrix the
+// same way exactly when their fingerprints agree)
+uint64_t plan_fingerprint(const Draft &d) {
+    uint64_t x = 1469598103934665603ULL;
+    auto mix = [&](const void *p, size_t n) {
+        const unsigned char *c = (const unsigned char *)p;
+        for (size_t i = 0; i < n; ++i) x = (x ^ c[i]) * 1099511628211ULL;
+    };
+    const Plan &p = d.pl;
+    const int64_t f[] = {p.k, p.kw, p.npanels, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
+                         p.xcd, p.lmax, p.exact_rows, p.ntile, p.tile_xcd, p.tile_wide, p.tile_mfma, p.tile_rows,
+                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse};
+    mix(f, sizeof(f));
+    mix(d.in.vrow_ptr.data(), d.in.vrow_ptr.size() * 4);
+    mix(d.in.vdest.data(), d.in.vdest.size() * 4);
+    mix(d.in.blk.data(), d.in.blk.size() * sizeof(int2));
+    mix(d.tp.tiles.data(), d.tp.tiles.size() * sizeof(int4));
+    mix(d.tp.chunks.data(), d.tp.chunks.size() * sizeof(int4));
+    return x;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1099,282 +1508,29 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     free_plan(h);
-
-    Plan pl;
-    pl.k = k;
-    // K panels of PANEL_ROW_BYTES-byte B rows when B would crowd the Infinity Cache and the B gather dominates the
-    // launch (>= 16 nonzeros per row); each extra panel re-streams A and cuts C rows into 256-B pieces, which only
-    // pays when it turns Infinity-Cache misses into hits (measured §6.2: config 2 K=128 1.65 ms at 32 columns vs
-    // 2.30 ms unpanelled; a 200 K-row, 10 nnz/row matrix with a 208 MB B is faster unpanelled).
-    const int panel_env = env_int("SPMM_HIP_PANEL_K", 0);
-    const double b_bytes = (double)h->ncols * k * (double)h->vsize;
-    const double avg_row = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
-    pl.kw = k;
-    if (h->var.panel_k > 0 || panel_env > 0) {
-        pl.kw = std::min(k, h->var.panel_k > 0 ? h->var.panel_k : panel_env);
-    } else if (b_bytes > PANEL_MIN_B_BYTES && avg_row >= PANEL_MIN_ROW_NNZ) {
-        pl.kw = std::min(k, std::max(1, (int)(PANEL_ROW_BYTES / h->vsize)));
-    }
-    // col_idx on the host (span, row similarity, windows, XCD order) when some policy below may need it
-    std::vector<int32_t> hcol;
-    double span = (double)h->ncols, crs = 1.0;
-    auto load_cols = [&]() -> int {
-        if (!hcol.empty() || h->nnz == 0) return SPMM_HIP_OK;
-        hcol.resize((size_t)h->nnz);
-        HIPCHK(hipMemcpy(hcol.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
-        span = mean_row_span(h->h_row_ptr.data(), hcol.data(), h->m);
-        crs = row_similarity_sample(h->h_row_ptr.data(), hcol.data(), h->m);
-        return SPMM_HIP_OK;
-    };
-    if (h->var.panel_k <= 0 && panel_env <= 0 && (double)pl.kw * h->vsize == 2.0 * WIN_LINE &&
-        avg_row >= NARROW_MIN_ROW && h->m > 1) {
-        if (int st = load_cols()) return st;
-        const double x = span * 2.0 * WIN_LINE / WIN_L2_BYTES;
-        if (crs < NARROW_MAX_CRS && x >= NARROW_MIN_SPAN_L2 && x <= NARROW_MAX_SPAN_L2) pl.kw /= 2;
-    }
-    pl.npanels = (k + pl.kw - 1) / pl.kw;
-    // block capacity and split length
-    int vec, g;
-    lane_layout(pl.kw, k, h->vsize, vec, g);
-    // block capacity: the LDS window (CAP), smaller for small matrices so >= ~1024 blocks exist (a 4096-nonzero
-    // window for one-lane row groups measured slower at K = 1, §6.2)
-    const int cap_env = env_int("SPMM_HIP_CAP", 0);
-    pl.cap = h->var.cap > 0 ? std::min(h->var.cap, CAP)
-             : cap_env > 0   ? std::min(cap_env, CAP)
-                             : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
-    const int seq_env = env_int("SPMM_HIP_SEQ_MAX", 0);
-    pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max : seq_env > 0 ? seq_env : split_length(h, pl.kw);
-    pl.seq_max = std::max(1, std::min(pl.seq_max, CAP));
-    pl.cap = std::max(pl.cap, std::min(CAP, pow2_ceil(pl.seq_max)));   // a row of T nonzeros fits one block
-    // rows per block: one row per row group when a group's row is long (>= 64 nonzeros) and a block of NG rows fits
-    // the LDS window -- the greedy packing would otherwise put NG + a few rows in a block and make a quarter of the
-    // groups run two rows while the rest idle (measured K=32, avg 100: 1.03-1.13x; avg 500 blocks hold < NG rows
-    // anyway; avg 20-50 unchanged or slower, r03_s2 / r03_s3 probes, DESIGN §6.13)
-    {
-        int vec_b, g_b;
-        lane_layout(pl.kw, k, h->vsize, vec_b, g_b);
-        const int ng = WG / g_b;
-        const int env_rows = env_int("SPMM_HIP_BLOCK_ROWS", 0);
-        pl.block_rows = CAP_ROWS;
-        if (env_rows > 0)
-            pl.block_rows = std::min(CAP_ROWS, env_rows);
-        else if (avg_row >= 64.0 && (double)ng * avg_row <= (double)pl.cap)
-            pl.block_rows = ng;
-    }
-
+    Draft d;
+    if (int st = draft_plan(h, k, nullptr, false, d)) return st;
+    const Plan &pl = d.pl;
+    TilePlan &tp = d.tp;
+    const bool tiles = d.tiles;
+    Inspection &in = d.in;
+    const int64_t W = d.W;
+    const std::vector<int32_t> &slot_lr = d.slot_lr;
     const int64_t srow_t = (int64_t)pl.kw * (int64_t)h->vsize;
-    // LDS B tiles (DESIGN §3.4): rows whose union of columns is reused enough leave the row kernel.  Needs 16-byte
-    // B pieces in every panel and sorted rows.  SPMM_HIP_TILES=-1 off / 1 every eligible tile; SPMM_HIP_TILE_REUSE
-    // sets the policy threshold.
-    TilePlan tp;
-    bool tiles = false;
-    {
-        const int64_t srow = srow_t;
-        const int env_t = env_int("SPMM_HIP_TILES", 0);
-        const int forced = h->var.tiles != 0 ? h->var.tiles : env_t;
-        int vec_t, g_t;
-        lane_layout(pl.kw, k, h->vsize, vec_t, g_t);
-        const bool shape_ok = h->nnz > 0 && vec_t == (int)(16 / h->vsize) && ((int64_t)k * h->vsize) % 16 == 0 &&
-                              srow % 16 == 0 && k % pl.kw == 0 && srow >= 64 && srow <= 1024 &&
-                              pow2_ceil(srow / 16) == srow / 16 &&
-                              h->ncols < INT32_MAX;
-        const int64_t win_forced = h->var.win_bytes != 0 ? h->var.win_bytes : (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
-        // matrix-core tiles first: fp64 32-column panels, strictly increasing columns, B < 4 GiB
-        const int env_m = env_int("SPMM_HIP_MFMA", 0);
-        const int fm = h->var.mfma != 0 ? h->var.mfma : env_m;
-        const bool mshape = fm >= 0 && h->vsize == 8 && pl.kw % 32 == 0 && k % 32 == 0 &&
-                            (double)h->ncols * (double)k * 8.0 < 4294967296.0;
-        if (forced >= 0 && h->nnz > 0 && h->ncols < INT32_MAX && win_forced <= 0 && (mshape || shape_ok)) {
-            if (int st = load_cols()) return st;
-            if (mshape && rows_strict(h->h_row_ptr.data(), hcol.data(), h->m)) {
-                const char *mthr = getenv("SPMM_HIP_MFMA_REUSE");
-                const bool force_m = forced > 0 || fm > 0;
-                const double mreuse = (mthr && *mthr) ? atof(mthr) : force_m ? 1.0 : MFMA_MIN_REUSE;
-                const double treuse = (mthr && *mthr) ? atof(mthr) : force_m ? 1.0 : MFMA_TILE_REUSE;
-                const double r16 = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max,
-                                                     MFMA_ROWS);
-                const bool menough = (h->m + MFMA_ROWS - 1) / MFMA_ROWS >= MFMA_MIN_TILES && h->nnz >= MFMA_MIN_NNZ;
-                if (force_m || (menough && r16 >= mreuse)) {
-                    tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, MFMA_ROWS,
-                                        MFMA_UC, MFMA_CAPA, treuse, tp);
-                    if (tiles && forced <= 0 && fm <= 0 && (int64_t)tp.tiles.size() < MFMA_MIN_TILES / 2) tiles = false;
-                    if (tiles && !tile_tables_fit(tp)) tiles = false;
-                    if (tiles) {
-                        pl.tile_mfma = 1;
-                        pl.tile_reuse = r16;
-                    }
-                }
-            }
-            if (!tiles && shape_ok && rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
-                const int rows_env = env_int("SPMM_HIP_TILE_ROWS", 0);
-                int rmax = std::min((WG / g_t) * tile_rpg(g_t), rows_env > 0 ? rows_env : TILE_ROWS);
-                const char *thr = getenv("SPMM_HIP_TILE_REUSE");
-                const double min_reuse = forced > 0 ? 1.0 : (thr && *thr) ? atof(thr) : TILE_MIN_REUSE;
-                pl.tile_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax);
-                const bool enough = (h->m + rmax - 1) / rmax >= TILE_MIN_TILES && srow <= TILE_POLICY_MAX_ROW;
-                if (forced > 0 || (enough && pl.tile_reuse >= min_reuse))
-                    tiles = build_tiles(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, rmax,
-                                        (int)(TILE_UCB / srow), TILE_CAPA, min_reuse, tp,
-                                        tile_colmax_for(h->vsize, g_t) - 4, TILE_DMAX - 1);
-                if (tiles && forced <= 0 && (int64_t)tp.tiles.size() < TILE_MIN_BUILT) tiles = false;
-                if (tiles && !tile_tables_fit(tp)) tiles = false;     // 32-bit tile positions (row kernel instead)
-            }
-        }
-        if (tiles) {
-            pl.ntile = (int)tp.tiles.size();
-            pl.tile_rows = tp.rows;
-            pl.tile_nnz = tp.nnz;
-            pl.tile_chunks = (int64_t)tp.chunks.size() - 1;
-            // consecutive tiles share most of their columns: in XCD order they share an L2 as well
-            const int env_x = env_int("SPMM_HIP_TILE_XCD", 1);
-            pl.tile_xcd = (env_x > 0 && pl.ntile >= 64) ? 1 : 0;
-            // compute-lane width in 16-byte pieces: the requested 1/2/4, lowered until rows per group divide
-            int sw = std::max(1, env_int("SPMM_HIP_TILE_WIDE", TILE_WIDE_DEFAULT));
-            sw = sw >= 2 ? 2 : 1;
-            while (sw > 1 && tile_rpg(g_t) % sw != 0) sw /= 2;
-            pl.tile_wide = sw;
-        }
-    }
-
-    // XCD-contiguous order, else column windows (chained mode; needs every row's columns sorted); both decided from
-    // col_idx on the host
-    Inspection in;
-    int64_t W = 0;
-    {
-        const double srow = (double)pl.kw * (double)h->vsize;
-        const int64_t env_bytes = (int64_t)env_int("SPMM_HIP_WIN_BYTES", 0);
-        const int64_t forced = h->var.win_bytes != 0 ? h->var.win_bytes : env_bytes;
-        const bool b_big = (double)h->ncols * std::max(srow, WIN_LINE) > WIN_MIN_SPAN_NARROW * WIN_L2_BYTES;
-        const bool maybe_win = h->nnz > 0 && forced >= 0 && (forced > 0 || (b_big && (srow >= WIN_MIN_ROW_BYTES || srow <= WIN_TINY_ROW_BYTES)));
-        const bool maybe_xcd = h->nnz > 0 && (double)h->ncols * srow > WIN_L2_BYTES;
-        if (maybe_win || maybe_xcd) {
-            if (int st = load_cols()) return st;
-        }
-        pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
-        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) &&
-            rows_sorted(h->h_row_ptr.data(), hcol.data(), h->m)) {
-            std::vector<Piece> pcs;
-            Inspection tmp;
-            make_pieces(h->h_row_ptr.data(), h->m, pl.seq_max, pcs, tmp);
-            W = window_cols(h, pl.kw, pcs, hcol.data(), h->var.win_bytes, crs, &pl.nseg);
-        }
-    }
-    if (W > 0) {
-        pl.xcd = 0;
-        inspect_windows(h->h_row_ptr.data(), hcol.data(), h->m, h->ncols, pl.seq_max, pl.cap, W, in, pl.block_rows);
-        pl.win_cols = W;
-        pl.nwin = (int)in.win_blk.size() - 1;
-        pl.nseg = (int64_t)in.vdest.size();
-    } else {
-        // when tiles hold nearly all the work, the row kernel's launch is only the leftover rows -- typically one
-        // skewed row of thousands of nonzeros whose T-pieces each run as a latency-bound serial chain (~64 us for
-        // 2,048 gathers) after the tile kernel: cut those rows into short pieces instead
-        if (tiles && pl.tile_mfma && (double)(h->nnz - tp.nnz) < GAP_SHORT_FRAC * (double)h->nnz && pl.seq_max > GAP_SEQ_MAX &&
-            h->var.seq_max <= 0 && env_int("SPMM_HIP_SEQ_MAX", 0) <= 0)
-            pl.seq_max = GAP_SEQ_MAX;
-        inspect(h->h_row_ptr.data(), h->m, pl.seq_max, pl.cap, in, /*heavy_first=*/!pl.xcd,
-                tiles ? tp.in_tile.data() : nullptr, pl.block_rows);
-        pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
-    }
     h->nv = (int64_t)in.vrow_ptr.size() - 1;
     h->nblk = (int)in.blk.size();
     h->nlong = (int)in.long_rows.size();
     h->nslots = in.nslots;
-    // vector lanes when the staged blocks hold fewer rows than row groups (long rows at small K; DESIGN §6.4), and
-    // the exact-row mask: rows <= T whose every virtual row sits in a block with L = 1
-    {
-        int vec, g;
-        lane_layout(pl.kw, k, h->vsize, vec, g);
-        const int ng = WG / g;
-        const int lcap = std::max(1, 64 / g);
-        // the rows the row kernel runs: gap virtual rows and the tile rows' nonzeros are not among them
-        const double nvr = (double)((int64_t)in.vrow_ptr.size() - 1 - in.ngaps);
-        const double nnz_rows = (double)(h->nnz - (tiles ? tp.nnz : 0));
-        const double rows_per_block = in.blk.empty() ? 0.0 : nvr / (double)in.blk.size();
-        const double mean_vrow = nvr > 0 ? nnz_rows / nvr : 0.0;
-        const int env_l = env_int("SPMM_HIP_LANES", 0);
-        const int forced = h->var.lanes != 0 ? h->var.lanes : env_l;
-        bool all_blocks = false;
-        if (forced != 0)
-            all_blocks = forced > 0, pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
-        else
-            all_blocks = nnz_rows > 0 && rows_per_block <= VL_ROW_FILL * ng && mean_vrow >= VL_MIN_ROW,
-            pl.lmax = all_blocks ? lcap : 1;
-        // flag the blocks that may use vector lanes: all of them under the policy, else (unless disabled) the blocks
-        // made only of split-row pieces (inexact anyway; a 16 M-nonzero row is thousands of one-piece blocks)
-        auto dest_of = [&](int v) -> int64_t {
-            if (in.vdest.empty()) return v;
-            return (W > 0) ? (in.vdest[v] >> 1) : in.vdest[v];
-        };
-        bool any_flag = false;
-        for (int2 &bk : in.blk) {
-            bool ok = all_blocks;
-            if (!ok && forced >= 0 && !in.long_rows.empty() && bk.y - bk.x < ng) {
-                ok = true;
-                for (int v = bk.x; v < bk.y && ok; ++v) ok = dest_of(v) < 0;
-            }
-            if (ok) bk.y |= BLK_VL_FLAG, any_flag = true;
-        }
-        if (any_flag && pl.lmax <= 1) pl.lmax = lcap;
-        h->exact.assign((size_t)h->m, 1);
-        for (const int4 &lr : in.long_rows) h->exact[(size_t)lr.x] = 0;
-        if (pl.lmax > 1) {
-            for (const int2 &bk : in.blk) {
-                if (!(bk.y & BLK_VL_FLAG)) continue;
-                const int e = bk.y & BLK_ROWS_MASK, nrows = e - bk.x;
-                if (nrows >= ng) continue;
-                int L = 1;
-                while (2 * L <= ng / nrows) L *= 2;
-                if (std::min(L, pl.lmax) <= 1) continue;
-                for (int v = bk.x; v < e; ++v) {
-                    const int64_t d = dest_of(v);
-                    if (d >= 0) h->exact[(size_t)d] = 0;
-                }
-            }
-        }
-        pl.exact_rows = 0;
-        for (uint8_t e : h->exact) pl.exact_rows += e;
-    }
-    // fused combine (DESIGN §3.2): split rows summed by the block that stores their last piece, so no combine
-    // launch.  Needs one launch per panel (no column windows), partials below 4 GiB (32-bit buffer offsets) and each
-    // split row's pieces in consecutive virtual rows with consecutive slots (what inspect() builds; checked here).
-    // SPMM_HIP_FUSE=0 keeps the separate spmm_combine_kernel.
-    std::vector<int32_t> slot_lr;
-    {
-        bool fuse = h->nslots > 0 && W == 0 && env_int("SPMM_HIP_FUSE", 1) != 0 &&
-                    (uint64_t)h->nslots * (uint64_t)k * h->vsize < (1ULL << 32);
-        if (fuse) {
-            slot_lr.assign((size_t)h->nslots, -1);
-            std::vector<int64_t> slot_v((size_t)h->nslots, -1);
-            for (size_t v = 0; v < in.vdest.size(); ++v)
-                if (in.vdest[v] < 0) slot_v[(size_t)(-in.vdest[v] - 1)] = (int64_t)v;
-            for (size_t li = 0; li < in.long_rows.size() && fuse; ++li) {
-                const int4 lr = in.long_rows[li];
-                for (int q = 0; q < lr.z && fuse; ++q) {
-                    const int sl = lr.y + q;
-                    fuse = sl < h->nslots && slot_v[(size_t)sl] >= 0 && slot_lr[(size_t)sl] < 0 &&
-                           (q == 0 || slot_v[(size_t)sl] == slot_v[(size_t)sl - 1] + 1);
-                    if (fuse) slot_lr[(size_t)sl] = (int32_t)li;
-                }
-            }
-            for (int32_t x : slot_lr) fuse = fuse && x >= 0;
-        }
-        if (fuse) {
-            for (int2 &bk : in.blk) {
-                const int e = bk.y & BLK_ROWS_MASK;
-                for (int v = bk.x; v < e; ++v)
-                    if (in.vdest[(size_t)v] < 0) {
-                        bk.y |= BLK_SPLIT_FLAG;
-                        break;
-                    }
-            }
-        }
-        h->fuse = fuse;
-        if (!fuse) slot_lr.clear();
-    }
+    h->exact.swap(d.exact);
+    h->fuse = d.fuse;
     h->plan = pl;
     h->win_blk = in.win_blk;
     h->win_v = in.win_v;
+    std::vector<int32_t> hcol;     // the tile / window copies below re-read the columns
+    if (W > 0) {
+        hcol.resize((size_t)h->nnz);
+        HIPCHK(hipMemcpy(hcol.data(), h->d_col, (size_t)h->nnz * 4, hipMemcpyDeviceToHost));
+    }
 
     auto alloc_copy = [&](void **dst, const void *src, size_t bytes) -> hipError_t {
         hipError_t e = hipMalloc(dst, std::max<size_t>(bytes, 4));
@@ -1460,13 +1616,21 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         }
     }
     if (e == hipSuccess && tiles && !pl.tile_mfma) {
-        // chunk-major copies of the tile rows' values and their chunk-local column indices (+ 64 B of padding)
+        // chunk-major copies of the tile rows' values and their chunk-local column indices (+ 64 B of padding).
+        // A padding entry is (value -0, the zero B row): fma(-0, +0, acc) == acc for every acc, -0 included (a +0
+        // value would turn a -0 chain, which the reference can reach through underflow, into +0)
         std::vector<char> hval((size_t)h->nnz * h->vsize);
         e = hipMemcpy(hval.data(), h->d_val, hval.size(), hipMemcpyDeviceToHost);
         const size_t nz = tp.perm.size();
         std::vector<char> tval(nz * h->vsize + PAD_BYTES, 0);
-        for (size_t q = 0; q < nz; ++q)
-            if (tp.perm[q] >= 0) std::memcpy(&tval[q * h->vsize], &hval[(size_t)tp.perm[q] * h->vsize], h->vsize);
+        const double mz64 = -0.0;
+        const float mz32 = -0.0f;
+        for (size_t q = 0; q < nz; ++q) {
+            if (tp.perm[q] >= 0)
+                std::memcpy(&tval[q * h->vsize], &hval[(size_t)tp.perm[q] * h->vsize], h->vsize);
+            else
+                std::memcpy(&tval[q * h->vsize], h->vsize == 8 ? (const void *)&mz64 : (const void *)&mz32, h->vsize);
+        }
         // chunk-local column -> byte offset of its row in the staged B image (padding: the zero row after the image)
         for (uint16_t &l : tp.tlidx) l = (l == TILE_PAD_LIDX) ? (uint16_t)TILE_UCB : (uint16_t)(l * srow_t);
         tp.tlidx.resize(nz + PAD_BYTES / 2, 0);
@@ -1626,7 +1790,7 @@ __global__ __launch_bounds__(WG) void gather_values_kernel(const T *__restrict__
     const int64_t q = (int64_t)blockIdx.x * WG + threadIdx.x;
     if (q < n) {
         const int32_t j = perm[q];
-        dst[q] = j >= 0 ? src[j] : T(0);
+        dst[q] = j >= 0 ? src[j] : T(-0.0);    // padding: -0 (LDS tiles: fma(-0, +0, acc) == acc, -0 kept)
     }
 }
 
@@ -1842,7 +2006,7 @@ int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out) {
 
 int spmm_hip_tile_mode(const spmm_hip_t *h) {
     if (!h) return fail(SPMM_HIP_ERR_ARG, "tile_mode: bad handle");
-    if (h->multi) return 0;
+    if (h->multi) return multi_tile_mode(h);
     return h->plan.ntile == 0 ? 0 : h->plan.tile_mfma ? 2 : 1;
 }
 
@@ -1914,6 +2078,61 @@ int spmm_hip_debug_inspect(const int32_t *row_ptr, const int32_t *col_idx, int64
     out->win_blk = dup(in.win_blk);
     out->long_rows = (int32_t *)dup(in.long_rows);
     out->perm = in.perm.empty() ? nullptr : dup(in.perm);
+    return SPMM_HIP_OK;
+}
+
+int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t k,
+                        int32_t dtype, int32_t mfma, int32_t gate_only, double *out) {
+    if (!row_ptr || !out || m < 0 || ncols < 0 || k < 1 || (dtype != SPMM_HIP_F64 && dtype != SPMM_HIP_F32))
+        return fail(SPMM_HIP_ERR_ARG, "debug_plan: bad arguments");
+    if (m >= INT32_MAX || ncols >= INT32_MAX) return fail(SPMM_HIP_ERR_OVERFLOW, "debug_plan: m, ncols must fit int32");
+    if (row_ptr[0] != 0) return fail(SPMM_HIP_ERR_CSR, "debug_plan: row_ptr[0] != 0");
+    for (int64_t i = 0; i < m; ++i)
+        if (row_ptr[i + 1] < row_ptr[i]) return fail(SPMM_HIP_ERR_CSR, "debug_plan: row_ptr not monotone");
+    const int64_t nnz = row_ptr[m];
+    if (nnz > 0 && !col_idx) return fail(SPMM_HIP_ERR_ARG, "debug_plan: col_idx NULL");
+    if (!gate_only)
+        for (int64_t j = 0; j < nnz; ++j)
+            if (col_idx[j] < 0 || col_idx[j] >= ncols) return fail(SPMM_HIP_ERR_CSR, "debug_plan: col_idx out of range");
+    spmm_hip_t h;                 // host-only view: no device state is touched
+    h.dtype = dtype;
+    h.vsize = dtype == SPMM_HIP_F64 ? 8 : 4;
+    h.m = m, h.ncols = ncols, h.nnz = nnz;
+    h.h_row_ptr.assign(row_ptr, row_ptr + m + 1);
+    h.var.mfma = mfma;
+    Draft d;
+    if (int st = draft_plan(&h, k, col_idx, gate_only != 0, d)) return st;
+    const Plan &p = d.pl;
+    for (int i = 0; i < SPMM_HIP_PLAN_SLOTS; ++i) out[i] = 0.0;
+    out[0] = d.gate_only ? (p.tile_mfma ? 2 : 0) : (p.ntile == 0 ? 0 : p.tile_mfma ? 2 : 1);
+    out[1] = d.gate.verdict;
+    out[2] = d.gate.r16;
+    out[3] = d.gate.take;
+    out[4] = d.gate.tile_nnz;
+    out[5] = d.gate.chunks;
+    out[6] = d.gate.max_chunks;
+    out[7] = d.gate.t_on;
+    out[8] = d.gate.t_off;
+    out[9] = d.gate.sampled;
+    out[10] = p.seq_max;
+    out[11] = p.piece;
+    out[12] = p.kw;
+    out[13] = p.npanels;
+    if (!d.gate_only) {
+        out[14] = p.ntile;
+        out[15] = (double)p.tile_nnz;
+        out[16] = (double)p.tile_chunks;
+        out[17] = (double)d.in.blk.size();
+        out[18] = (double)d.in.long_rows.size();
+        out[19] = (double)p.exact_rows;
+        out[20] = p.lmax;
+        out[21] = p.xcd;
+        out[22] = p.nwin;
+        const uint64_t fp = plan_fingerprint(d);
+        out[24] = (double)(fp & 0xFFFFFFFFull);
+        out[25] = (double)(fp >> 32);
+    }
+    out[23] = d.gate_only ? 1 : 0;
     return SPMM_HIP_OK;
 }
 

@@ -33,7 +33,8 @@ int fail(int status, const std::string &what);  // records the detail, returns s
 struct Plan {
     int k = -1;
     int kw = 0, npanels = 0;   // panel width (columns) and count
-    int seq_max = 0;           // T
+    int seq_max = 0;           // T: rows of <= T nonzeros are one chain (exact)
+    int piece = 0;             // rows longer than T are cut into pieces of this many nonzeros (T, or GAP_SEQ_MAX)
     int cap = 0;               // block capacity (nonzeros)
     int block_rows = 512;      // virtual rows per block at most (CAP_ROWS; SPMM_HIP_BLOCK_ROWS lowers it)
     int64_t win_cols = 0;      // column-window width (0 = one window over all columns)
@@ -74,6 +75,7 @@ int multi_run_device(spmm_hip_t *h, const void *d_b, int layout, void *d_c, int 
 int multi_update_values(spmm_hip_t *h, const void *vals, bool device, hipStream_t s);
 int multi_last_times(spmm_hip_t *h, double *out_ms);
 void multi_info(const spmm_hip_t *h, int64_t *out);
+int multi_tile_mode(const spmm_hip_t *h);
 void multi_destroy(spmm_hip_t *h);
 
 }  // namespace spmm_engine

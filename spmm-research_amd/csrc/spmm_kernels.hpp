@@ -430,8 +430,9 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
 // inspector lists the union U of their columns (sorted) and cuts it into CHUNKS of <= UCB bytes of B rows and <=
 // CAPA entries.  Per chunk the workgroup stages (through VGPRs) the chunk's B rows and the chunk's entries from a
 // chunk-major copy of A: values and 16-bit byte offsets of their B rows in the staged image, row by row, each
-// row's segment padded to a multiple of 4 entries with (value +0, the all-zero B row) -- fma(+0, +0, acc) == acc
-// exactly because a chain that starts from +0 can never hold -0 -- so the inner loop reads 4 offsets and 4 values
+// row's segment padded to a multiple of 4 entries with (value -0, the all-zero B row) -- fma(-0, +0, acc) == acc
+// exactly for every acc, -0 included (a chain can reach -0 through an underflowing product) -- so the inner loop
+// reads 4 offsets and 4 values
 // per step with no predication.  Row group g (G lanes, VEC columns each) owns rows g, g+NG, ... of the tile and
 // carries their accumulators in registers across chunks; chunks go in column order and each row's columns are
 // sorted, so every row is still ONE fused multiply-add chain from 0 in CSR order -- bit-identical to the

@@ -329,6 +329,13 @@ void multi_info(const spmm_hip_t *h, int64_t *out) {
     out[18] = fuse;
 }
 
+// The tile kernel the shards run: 2 when any shard runs matrix-core tiles, else 1 when any runs LDS tiles, else 0.
+int multi_tile_mode(const spmm_hip_t *h) {
+    int mode = 0;
+    for (const spmm_hip_t *c : h->multi->shard) mode = std::max(mode, spmm_hip_tile_mode(c));
+    return mode;
+}
+
 void multi_destroy(spmm_hip_t *h) {
     MultiState *M = h->multi;
     if (!M) return;

@@ -441,6 +441,77 @@ int spmm_host_generate_rows(const spmm_gen_params_t *p, int64_t r0, int64_t r1, 
     return SPMM_HOST_OK;
 }
 
+// The whole matrix's row_ptr with the columns (and values) of the rows where mask[i] != 0 only -- the other rows'
+// entries are left zero (column 0).  Only the 4096-row copy-chain segments that hold a masked row are generated, up
+// to their last masked row, so a row sample of a large matrix costs a fraction of the full generation
+// (tools/plan_census.py: the matrix-core gate reads its sampled 16-row tiles only).  The masked rows are identical to
+// the same rows of spmm_host_generate.
+int spmm_host_generate_masked(const spmm_gen_params_t *p, const uint8_t *mask, spmm_csr_t *out) {
+    if (!valid(p) || !out || !mask) return SPMM_HOST_ERR_ARG;
+    memset(out, 0, sizeof(*out));
+    std::vector<int64_t> deg;
+    int st = row_degrees(p, deg);
+    if (st) return st;
+    const int64_t m = p->nr_rows;
+    int64_t nnz = 0;
+    for (int64_t i = 0; i < m; ++i) nnz += deg[i];
+    out->m = m;
+    out->ncols = p->nr_cols;
+    out->nnz = nnz;
+    out->row_ptr = (int32_t *)malloc((size_t)(m + 1) * sizeof(int32_t));
+    out->col_idx = (int32_t *)calloc((size_t)std::max<int64_t>(nnz, 1), sizeof(int32_t));   // untouched pages stay
+    out->values = (double *)calloc((size_t)std::max<int64_t>(nnz, 1), sizeof(double));     // unmapped
+    if (!out->row_ptr || !out->col_idx || !out->values) {
+        spmm_host_csr_free(out);
+        return SPMM_HOST_ERR_NOMEM;
+    }
+    out->row_ptr[0] = 0;
+    for (int64_t i = 0; i < m; ++i) out->row_ptr[i + 1] = (int32_t)(out->row_ptr[i] + deg[i]);
+    int64_t multi = 0;   // as fill_rows: rows with >= 2 nonzeros over the whole matrix
+    for (int64_t d : deg) multi += (d >= 2);
+    const double bw_scale = 1.0 / std::max(0.05, (double)multi / (double)std::max<size_t>(deg.size(), 1));
+    std::vector<int64_t> segs;
+    for (int64_t s = 0; s * SEG < m; ++s) {
+        const int64_t a = s * SEG, b = std::min<int64_t>((s + 1) * SEG, m);
+        for (int64_t i = a; i < b; ++i)
+            if (mask[i]) {
+                segs.push_back(s);
+                break;
+            }
+    }
+#pragma omp parallel
+    {
+        RowGen g;
+        g.p = p;
+        g.bw_scale = bw_scale;
+#pragma omp for schedule(dynamic, 1)
+        for (size_t q = 0; q < segs.size(); ++q) {
+            g.prev.clear();
+            g.runs_prev.clear();
+            const int64_t a = segs[q] * SEG, b = std::min<int64_t>((segs[q] + 1) * SEG, m);
+            int64_t last = a;
+            for (int64_t i = a; i < b; ++i)
+                if (mask[i]) last = i + 1;
+            for (int64_t i = a; i < last; ++i) {
+                g.gen(i, deg[i]);
+                if (mask[i]) {
+                    const int64_t base = out->row_ptr[i];
+                    Rng rv((uint64_t)p->seed, (uint64_t)i, S_VALS);
+                    for (size_t t = 0; t < g.cur.size(); ++t) {
+                        out->col_idx[base + t] = g.cur[t];
+                        out->values[base + t] = 0.5 + rv.uniform();
+                    }
+                }
+                if (!g.cur.empty()) {
+                    std::swap(g.prev, g.cur);
+                    std::swap(g.runs_prev, g.runs_cur);
+                }
+            }
+        }
+    }
+    return SPMM_HOST_OK;
+}
+
 int spmm_host_generate(const spmm_gen_params_t *p, spmm_csr_t *out) {
     if (!valid(p)) return SPMM_HOST_ERR_ARG;
     return spmm_host_generate_rows(p, 0, p->nr_rows, out);

@@ -141,6 +141,7 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
                                        C.POINTER(_Tiles)]
     L.spmm_hip_debug_tiles_free.argtypes = [C.POINTER(_Tiles)]
     L.spmm_hip_debug_tiles_free.restype = None
+    L.spmm_hip_debug_plan.argtypes = [_i32p, _i32p, i64, i64, i32, i32, i32, i32, _f64p]
     L.spmm_hip_strerror.argtypes = [C.c_int]
     L.spmm_hip_strerror.restype = C.c_char_p
     L.spmm_hip_last_error_detail.restype = C.c_char_p
@@ -155,6 +156,8 @@ def _bind_host(L: C.CDLL) -> C.CDLL:
     L.spmm_host_generate.argtypes = [C.POINTER(_GenParams), C.POINTER(_CSRStruct)]
     L.spmm_host_generate_row_ptr.argtypes = [C.POINTER(_GenParams), _i32p]
     L.spmm_host_generate_rows.argtypes = [C.POINTER(_GenParams), i64, i64, C.POINTER(_CSRStruct)]
+    L.spmm_host_generate_masked.argtypes = [C.POINTER(_GenParams), np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"),
+                                            C.POINTER(_CSRStruct)]
     L.spmm_host_features.argtypes = [C.POINTER(_CSRStruct), C.POINTER(_Features)]
     L.spmm_host_mtx_read.argtypes = [C.c_char_p, C.POINTER(_CSRStruct), C.c_char_p, C.c_int, C.POINTER(C.c_int32)]
     L.spmm_host_smtx_read.argtypes = [C.c_char_p, i64, C.POINTER(_CSRStruct)]
@@ -235,6 +238,15 @@ def generate_row_ptr(params: _GenParams) -> np.ndarray:
 def generate_rows(params: _GenParams, r0: int, r1: int) -> CSR:
     s = _CSRStruct()
     st = host.spmm_host_generate_rows(C.byref(params), r0, r1, C.byref(s))
+    if st != 0:
+        raise RuntimeError(f"generator failed ({st})")
+    return _take_csr(s)
+
+
+def generate_masked(params: _GenParams, mask: np.ndarray) -> CSR:
+    """The whole matrix's row_ptr with the columns / values of the rows where mask is set only (others zero)."""
+    s = _CSRStruct()
+    st = host.spmm_host_generate_masked(C.byref(params), np.ascontiguousarray(mask, np.uint8), C.byref(s))
     if st != 0:
         raise RuntimeError(f"generator failed ({st})")
     return _take_csr(s)
@@ -366,6 +378,38 @@ def debug_tiles(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, T: int, rm
     finally:
         hip.spmm_hip_debug_tiles_free(C.byref(t))
     return out
+
+
+PLAN_SLOTS = 32     # SPMM_HIP_PLAN_SLOTS
+PLAN_FIELDS = ("mode", "gate", "r16", "take", "est_tile_nnz", "est_chunks", "max_chunks", "t_on_us", "t_off_us",
+               "sampled", "seq_max", "piece", "kw", "npanels", "ntile", "tile_nnz", "tile_chunks", "blocks",
+               "split_rows", "exact_rows", "lmax", "xcd", "nwin", "gate_only", "fp_lo", "fp_hi")
+
+
+def debug_plan(row_ptr: np.ndarray, col_idx: np.ndarray, ncols: int, k: int, dtype: int = F64, mfma: int = 0,
+               gate_only: bool = False) -> dict:
+    """What spmm_hip_plan decides for (CSR, k, dtype), on the host (spmm_hip_debug_plan): tile mode, the matrix-core
+    gate's sample and cost model, the plan's shape and a fingerprint of its tables.  mfma: the SPMM_HIP_MFMA override;
+    gate_only: stop after the gate (col_idx only needs the gate's sampled rows, see gate_sample_rows)."""
+    rp = np.ascontiguousarray(row_ptr, np.int32)
+    ci = np.ascontiguousarray(col_idx if len(col_idx) else np.zeros(1), np.int32)
+    out = np.zeros(PLAN_SLOTS, np.float64)
+    _check("debug_plan", hip.spmm_hip_debug_plan(rp, ci, len(rp) - 1, ncols, k, dtype, mfma, int(gate_only), out))
+    d = {f: float(out[i]) for i, f in enumerate(PLAN_FIELDS)}
+    d["mode"] = {0: "none", 1: "lds", 2: "mfma"}[int(out[0])]
+    d["fingerprint"] = int(out[25]) << 32 | int(out[24])
+    return d
+
+
+def gate_sample_rows(m: int) -> np.ndarray:
+    """bool[m]: the rows of the matrix-core gate's sampled 16-row tiles (include/spmm_hip.h, spmm_hip_debug_plan)."""
+    mask = np.zeros(m, np.uint8)
+    nt = (m + 15) // 16
+    ns = min(256, nt)
+    for i in range(ns):
+        t = i * nt // ns
+        mask[t * 16:min(m, t * 16 + 16)] = 1
+    return mask
 
 
 def device_count() -> int:

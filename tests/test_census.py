@@ -1,0 +1,78 @@
+"""CPU tests of the host-only planner (spmm_hip_debug_plan) and the dataset census built on it (tools/plan_census.py).
+
+The census evaluates the matrix-core gate of every medium-dataset line from the gate's sampled
+16-row tiles only: the matrix is generated for those rows (spmm_host_generate_masked) and the gate must decide
+exactly as it does on the full matrix.  A line the gate keeps off must plan exactly as the engine without
+matrix-core tiles (SPMM_HIP_MFMA=-1: the config-3 sweep build's plan) -- same plan fingerprint.
+"""
+import numpy as np
+import pytest
+
+LINES = ["22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14",      # dense band: tiles
+         "39120 39120 500 166.6667 normal random 0.05 0 0.05 0.5 14",
+         "111476 111476 100 33.3333 normal random 0.3 0 0.5 0.95 14",
+         "250000 250000 20 6.6667 normal random 0.3 100 0.95 0.5 14",       # config-2-like: no tiles
+         "4000 4000 40 13 normal random 0.6 0 0.05 0.05 14"]
+
+
+@pytest.fixture(scope="module")
+def S():
+    import spmm_amd
+    return spmm_amd
+
+
+@pytest.mark.parametrize("line", LINES)
+def test_masked_generation_equals_full(S, line):
+    p = S.gen_params(line)
+    A = S.generate(p)
+    mask = S.gate_sample_rows(A.m)
+    M = S.generate_masked(p, mask)
+    assert np.array_equal(M.row_ptr, A.row_ptr)
+    sel = np.repeat(mask.astype(bool), np.diff(A.row_ptr))
+    assert np.array_equal(M.col_idx[sel], A.col_idx[sel]) and np.array_equal(M.values[sel], A.values[sel])
+
+
+@pytest.mark.parametrize("line", LINES)
+@pytest.mark.parametrize("k", [32, 128])
+def test_gate_from_sample_equals_full(S, line, k):
+    """The gate reads its sampled rows only: masked columns and full columns give the same decision and statistics,
+    and the full plan takes matrix-core tiles exactly when the gate says so."""
+    p = S.gen_params(line)
+    A = S.generate(p)
+    M = S.generate_masked(p, S.gate_sample_rows(A.m))
+    g_full = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, gate_only=True)
+    g_mask = S.debug_plan(M.row_ptr, M.col_idx, M.ncols, k, gate_only=True)
+    for f in ("mode", "gate", "r16", "take", "est_tile_nnz", "est_chunks", "t_on_us", "t_off_us", "seq_max"):
+        assert g_full[f] == g_mask[f], f
+    full = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k)
+    assert (full["mode"] == "mfma") == (g_full["mode"] == "mfma")
+    off = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, mfma=-1)
+    assert off["mode"] != "mfma"
+    # unchanged vs the plan without matrix-core tiles exactly when the gate is off
+    assert (full["fingerprint"] == off["fingerprint"]) == (full["mode"] != "mfma")
+
+
+def test_debug_plan_estimates(S):
+    """The gate's sample estimates the built tiles: nonzeros in tiles within 5 %, chunks within 10 %."""
+    A = S.generate(S.gen_params(LINES[0]))
+    d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32)
+    assert d["mode"] == "mfma"
+    assert abs(d["est_tile_nnz"] / d["tile_nnz"] - 1) < 0.05
+    assert abs(d["est_chunks"] / d["tile_chunks"] - 1) < 0.10
+
+
+def test_debug_plan_forced_modes(S):
+    A = S.generate(S.gen_params(LINES[4]))
+    assert S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, mfma=1)["mode"] == "mfma"
+    assert S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, mfma=-1)["mode"] != "mfma"
+    f32 = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, dtype=S.F32, mfma=1)
+    assert f32["mode"] != "mfma"                         # fp32 never takes the f64 matrix-core tiles
+    assert S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 8, mfma=1)["mode"] != "mfma"   # K not a multiple of 32
+
+
+def test_debug_plan_rejects_bad_input(S):
+    rp = np.array([0, 2, 1], np.int32)
+    with pytest.raises(S.SpmmHipError):
+        S.debug_plan(rp, np.zeros(2, np.int32), 4, 32)
+    with pytest.raises(S.SpmmHipError):
+        S.debug_plan(np.array([0, 1], np.int32), np.array([7], np.int32), 4, 32)

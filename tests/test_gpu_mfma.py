@@ -8,6 +8,8 @@ reports exact must be BIT-IDENTICAL to the oracle and to the row kernel (SPMM_HI
 nothing more), value updates, duplicate columns / fp32 / narrow panels (refused: another kernel runs), the default
 policy on a dense band, and a captured hipGraph replay.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -164,3 +166,154 @@ def test_mfma_graph_replay(env, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(C1.view(torch.int64), C2.view(torch.int64))
     mf.close()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# IEEE edge cases (spmm_mfma.hpp header: the exact-chain range check).  The reference sums each row as one chain of
+# fused multiply-adds from +0 in IEEE double on x86 (spmm_kernel_csr.cpp:87-91): subnormal operands and products,
+# underflow to -0, -0 inputs and overflow all follow IEEE there.  A matrix-core tile adds fma(0, b, acc) steps for
+# its empty panel cells, which could turn a -0 chain into +0 and which would expose a flush-to-zero of subnormals;
+# the kernel therefore recomputes any tile whose operands leave 2^-458 <= |x| <= 2^500 by the sparse IEEE chain.
+# Rows the engine reports exact must be bit-identical to the oracle for every kind of value below, with matrix-core
+# tiles forced, with the LDS tile kernel forced (padding entries -0 on the zero B row) and with the row kernel.
+
+def edge_values(kind, n, rng):
+    """(A values, B values) of one edge-case family; n = (nnz, B entries)."""
+    na, nb = n
+    sa = rng.choice([-1.0, 1.0], na)
+    sb = rng.choice([-1.0, 1.0], nb)
+    ua, ub = rng.uniform(0.5, 1.5, na), rng.uniform(0.5, 1.5, nb)
+    if kind == "subnormal_a":        # A subnormal (2^-1070 .. 2^-1030), B ~ 1 .. 2^60: products subnormal or normal
+        return sa * ua * 2.0 ** rng.integers(-1070, -1030, na), sb * ub * 2.0 ** rng.integers(0, 60, nb)
+    if kind == "subnormal_b":
+        return sa * ua * 2.0 ** rng.integers(0, 60, na), sb * ub * 2.0 ** rng.integers(-1070, -1030, nb)
+    if kind == "underflow":          # products ~ 2^-1040 .. 2^-1090: subnormal partial sums, underflow to +-0
+        return sa * ua * 2.0 ** rng.integers(-545, -520, na), sb * ub * 2.0 ** rng.integers(-545, -520, nb)
+    if kind == "negzero":            # -0 / +0 entries and tiny negative products: -0 chains
+        a = sa * ua * 2.0 ** -540
+        b = sb * ub * 2.0 ** -540
+        a[rng.random(na) < 0.3] = -0.0
+        b[rng.random(nb) < 0.3] = -0.0
+        a[rng.random(na) < 0.1] = 0.0
+        return a, b
+    if kind == "near_range":         # just inside / outside the exact range bounds 2^-458, 2^500
+        return sa * 2.0 ** rng.choice([-459, -458, -457, 0, 499, 500], na), sb * 2.0 ** rng.choice([-459, -458, 0, 1], nb)
+    if kind == "overflow":           # products beyond DBL_MAX: +-Inf, Inf - Inf = NaN
+        return sa * ua * 2.0 ** rng.integers(480, 530, na), sb * ub * 2.0 ** rng.integers(480, 530, nb)
+    if kind == "mixed":              # per entry one of normal / tiny / zero / -0 / subnormal
+        a, b = sa * ua, sb * ub
+        for v in (a, b):
+            c = rng.integers(0, 5, len(v))
+            v[c == 1] *= 2.0 ** -1060
+            v[c == 2] *= 2.0 ** -530
+            v[c == 3] = 0.0
+            v[c == 4] = -0.0
+        return a, b
+    raise ValueError(kind)
+
+
+EDGE_KINDS = ["subnormal_a", "subnormal_b", "underflow", "negzero", "near_range", "overflow", "mixed"]
+EDGE_PLANS = {"mfma": {"SPMM_HIP_MFMA": "1"}, "lds": {"SPMM_HIP_MFMA": "-1", "SPMM_HIP_TILES": "1"},
+              "rows": {"SPMM_HIP_TILES": "-1"}}
+
+
+def same_bits_or_nan(got, want):
+    """Bit-identical, except that a NaN only has to be a NaN (x86 and the GPU make NaNs with different sign bits)."""
+    gn, wn = np.isnan(got), np.isnan(want)
+    return np.array_equal(gn, wn) and np.array_equal(bits(got[~gn]), bits(want[~wn]))
+
+
+@pytest.mark.parametrize("kind", EDGE_KINDS)
+@pytest.mark.parametrize("plan", list(EDGE_PLANS))
+@pytest.mark.parametrize("k", [32, 64])
+def test_edge_values_exact(env, monkeypatch, kind, plan, k):
+    torch, S, O = env
+    A = S.generate(S.gen_params(MATS[0]))
+    rng = np.random.default_rng(zlib.crc32(f"{kind}/{k}".encode()))
+    vals, x = edge_values(kind, (A.nnz, A.ncols * k), rng)
+    y, t, ex = run(S, A, vals, x, k, monkeypatch, EDGE_PLANS[plan])
+    if plan == "mfma":
+        assert t["mode"] == "mfma" and t["rows"] > 0.9 * A.m
+    elif plan == "lds":
+        assert t["mode"] == "lds" and t["rows"] > 0.5 * A.m
+    else:
+        assert t["tiles"] == 0
+    want = O.spmm(A.row_ptr, A.col_idx, vals, A.ncols, x, k)
+    assert ex.sum() > 0.99 * A.m
+    assert same_bits_or_nan(y[ex], want[ex]), f"{kind}: {plan} rows differ from the reference chain"
+    if kind in ("underflow", "negzero", "mixed"):          # the family really exercised signed zeros / subnormals
+        z = want[ex]
+        assert (np.signbit(z) & (z == 0)).any() or (np.abs(z[z != 0]) < 2.0 ** -1022).any()
+
+
+def test_mfma_edge_tile_only_falls_back(env, monkeypatch):
+    """One tiny B value makes only the tiles that read it take the sparse chain: all rows still exact and equal."""
+    torch, S, O = env
+    A = S.generate(S.gen_params(MATS[1]))
+    k = 32
+    x = O.drand48(11, A.ncols * k) * 2.0 - 1.0
+    x[5] = 2.0 ** -1070                      # one subnormal in B column 5 (column-major: x[n][col], n = 0)
+    x[7 * A.ncols + 40] = -0.0
+    y, t, ex = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    assert t["mode"] == "mfma"
+    want = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+    assert np.array_equal(bits(y[ex]), bits(want[ex]))
+
+
+def test_mfma_leftover_rows_keep_exactness(env, monkeypatch):
+    """ When tiles hold nearly all nonzeros only the rows longer than T are cut into 64-nonzero pieces: the
+    exact-row mask equals the plan without matrix-core tiles, and those rows equal the oracle."""
+    torch, S, O = env
+    A = S.generate(S.gen_params("6000 6000 100 33 normal random 0.05 60 0.95 0.95 14"))
+    k = 32
+    x = O.drand48(2, A.ncols * k)
+    y1, t1, ex1 = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    y0, t0, ex0 = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_TILES": "-1"})
+    assert t1["mode"] == "mfma" and t1["nnz"] > 0.875 * A.nnz
+    assert (~ex0).sum() >= 1                                 # the skewed row is split in both plans
+    assert np.array_equal(ex1, ex0)
+    want = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+    assert np.array_equal(bits(y1[ex1]), bits(want[ex1]))
+    g, absdot = O.gold(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+    assert O.normwise_ok(y1[~ex1], g[~ex1], absdot[~ex1], 1e-10).all()
+
+
+@pytest.mark.parametrize("np_env", ["1", "2"])
+def test_mfma_wave_panels_bitexact(env, monkeypatch, np_env):
+    """64-column waves (NP = 2) and 32-column waves give the same bits at K = 64, 96, 128, 160."""
+    torch, S, O = env
+    A = S.generate(S.gen_params(MATS[0]))
+    monkeypatch.setenv("SPMM_HIP_MFMA_NP", np_env)
+    for k in (64, 96, 160):
+        x = O.drand48(k, A.ncols * k) * 2.0 - 1.0
+        y, t, ex = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+        assert t["mode"] == "mfma"
+        want = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+        assert np.array_equal(bits(y[ex]), bits(want[ex])), k
+
+
+def test_multi_handle_tile_mode(env, monkeypatch):
+    """ A multi-GPU handle reports the tile kernel its shards run."""
+    torch, S, O = env
+    monkeypatch.setenv("SPMM_HIP_MFMA", "1")
+    A = S.generate(S.gen_params(MATS[0]))
+    mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, 32, 0, devices=[0, 0])
+    ti = mf.tile_info()
+    assert ti["tiles"] > 0 and ti["mode"] == "mfma"
+    mf.close()
+
+
+def test_debug_plan_matches_handle(env, monkeypatch):
+    """spmm_hip_debug_plan (host only) reports what the handle planned."""
+    torch, S, O = env
+    for kk in ("SPMM_HIP_TILES", "SPMM_HIP_MFMA", "SPMM_HIP_MFMA_REUSE"):
+        monkeypatch.delenv(kk, raising=False)
+    for line in ("22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14", MATS[2]):
+        A = S.generate(S.gen_params(line))
+        for k in (32, 128):
+            d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k)
+            mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0)
+            ti, inf = mf.tile_info(), mf.info()
+            assert d["mode"] == ti["mode"] and d["ntile"] == ti["tiles"] and d["tile_nnz"] == ti["nnz"]
+            assert d["seq_max"] == inf[8] and d["blocks"] == inf[5] and d["exact_rows"] == inf[17]
+            mf.close()

@@ -2,7 +2,7 @@
 
 A tile row must still be ONE left-to-right FMA chain over the row in CSR order (reference compute_csr,
 spmm_kernel_csr.cpp:70-96): chunk by chunk in column order, the row's segments concatenated must be exactly its CSR
-range, and every staged column must be the column of the nonzero that reads it (padding entries -- value +0 on
+range, and every staged column must be the column of the nonzero that reads it (padding entries -- value -0 on
 the zero B row -- only at the end of a segment, which is a multiple of 4 entries).  These invariants, plus the LDS
 limits the kernel relies on (<= uc columns and <= capa nonzeros per chunk, 8-aligned offsets), are what the GPU
 parity tests (tests/test_gpu_tiles.py) then confirm bit for bit.

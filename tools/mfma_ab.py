@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--budget", type=float, default=1e9, help="seconds; no new line after this")
+    ap.add_argument("--modes", default="off:SPMM_HIP_MFMA=-1;on:",
+                    help="';'-separated name:ENV=V,ENV=V handles to compare (the first is the baseline)")
     args = ap.parse_args()
     import torch
     import spmm_amd as S
@@ -56,7 +58,11 @@ def main():
             g.manual_seed(42)
             B = torch.rand((A.ncols, k), generator=g, device=dev, dtype=torch.float64) * 2 - 1
             hs = {}
-            for name, env in (("off", {"SPMM_HIP_MFMA": "-1"}), ("on", {})):
+            modes = []
+            for spec in args.modes.split(";"):
+                name, _, kv = spec.partition(":")
+                modes.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+            for name, env in modes:
                 for kk, vv in env.items():
                     os.environ[kk] = vv
                 hs[name] = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0)
@@ -74,17 +80,18 @@ def main():
                     e1.record(stream)
                     torch.cuda.synchronize()
                     ts[n].append(e0.elapsed_time(e1) / args.iters)
-            ex = torch.from_numpy(hs["off"].exact_rows() & hs["on"].exact_rows()).to(dev)
-            same = bool(torch.equal(Cs["on"][ex].view(torch.int64), Cs["off"][ex].view(torch.int64)))
-            ti = hs["on"].tile_info()
+            n0, n1 = modes[0][0], modes[-1][0]
+            ex = torch.from_numpy(hs[n0].exact_rows() & hs[n1].exact_rows()).to(dev)
+            same = all(bool(torch.equal(Cs[n][ex].view(torch.int64), Cs[n0][ex].view(torch.int64))) for n in hs)
+            ti = hs[n1].tile_info()
             ba = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64)
-            t_off, t_on = min(ts["off"]), min(ts["on"])
+            t_off, t_on = min(ts[n0]), min(ts[n1])
             rec = {"gen": line, "k": k, "m": A.m, "nnz": A.nnz, "off_ms": round(t_off, 5), "on_ms": round(t_on, 5),
                    "speedup": round(t_off / t_on, 3), "mode": ti["mode"], "tile_rows": ti["rows"],
-                   "chunks": ti["chunks"], "reuse": ti["reuse"],
+                   "tile_nnz": ti["nnz"], "chunks": ti["chunks"], "reuse": ti["reuse"],
                    "frac_off": round(ba / (t_off * 1e-3) / 8e12, 4), "frac_on": round(ba / (t_on * 1e-3) / 8e12, 4),
                    "gflops_on": round(2.0 * A.nnz * k / t_on / 1e6, 1), "exact_rows_both": int(ex.sum().item()),
-                   "bitexact": same}
+                   "bitexact": same, "ms": {n: round(min(ts[n]), 5) for n in ts}}
             print(json.dumps(rec), flush=True)
             for h in hs.values():
                 h.close()
