@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: test mode, ranks may share one GPU (collectives staged through host memory)")
     ap.add_argument("--dump-c", default=None, help="rank 0 writes a row sample of the (gathered) C + exact mask (npz)")
+    ap.add_argument("--no-multi-handle", action="store_true",
+                    help="N>1: skip the in-process multi-GPU handle record (peer vs RCCL B broadcast)")
     ap.add_argument("--no-dataset", action="store_true", help="skip the medium-dataset sub-record (N=1)")
     ap.add_argument("--dataset-stride", type=int, default=160, help="dataset: every n-th medium-dataset line")
     ap.add_argument("--dataset-offset", type=int, default=0)
@@ -576,6 +578,75 @@ def run_pipeline(args, torch, S, np):
     return 0 if ok else 1
 
 
+def run_multi_handle(args, torch, S, np, p, K: int, npdtype, B, Bh, devices: list, stream) -> dict:
+    """The C-ABI multi-GPU handle in ONE process (spmm_hip_create_multi, include/spmm_hip.h) -- the path the
+    reference-harness plugin takes with SPMM_HIP_NGPUS (integration/spmm_kernel_hip.cpp) -- over the same global
+    matrix and the same reference-partitioner shards as the torch.distributed ranks.  B (on device 0) is replicated
+    once by each broadcast the handle offers, side by side (SURVEY §8e "benchmark both"): root -> peer
+    hipMemcpyPeerAsync over xGMI, and one grouped RCCL broadcast (SPMM_HIP_BCAST=rccl, distinct devices only); then
+    spmm_hip_run_sharded is timed with HIP events on the caller's stream (every shard's stream forks from it and joins
+    back into it), C left sharded like the distributed loop.  Afterwards C is gathered to device 0 once
+    (spmm_hip_run_device) and self-checked.  Rank 0 only, after the distributed measurement."""
+    A = S.generate(p)
+    flops = 2.0 * A.nnz * K
+    bbytes = float(A.ncols) * K * np.dtype(npdtype).itemsize
+    ndist = len(set(devices))
+    sp = stream.cuda_stream
+    out = {"devices": devices, "nnz": int(A.nnz), "b_bytes": bbytes, "modes": {}}
+
+    def sync_all():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+    for mode in ("peer", "rccl"):
+        if mode == "rccl" and ndist != len(devices):
+            out["modes"][mode] = {"skipped": "RCCL broadcast needs distinct devices (shards share a GPU in this run)"}
+            continue
+        old = os.environ.get("SPMM_HIP_BCAST")
+        os.environ.pop("SPMM_HIP_BCAST", None)
+        if mode == "rccl":
+            os.environ["SPMM_HIP_BCAST"] = "rccl"
+        try:
+            mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdtype), A.m, A.ncols, A.nnz, K,
+                                 devices=devices)
+        except S.SpmmHipError as e:
+            out["modes"][mode] = {"skipped": str(e)}
+            continue
+        finally:
+            os.environ.pop("SPMM_HIP_BCAST", None)
+            if old is not None:
+                os.environ["SPMM_HIP_BCAST"] = old
+        mf.broadcast_b(B.data_ptr(), S.B_ROW_MAJOR, K, sp)
+        sync_all()
+        tb = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            mf.broadcast_b(B.data_ptr(), S.B_ROW_MAJOR, K, sp)
+            sync_all()
+            tb.append(time.perf_counter() - t0)
+        t_b = sorted(tb)[2]
+        for _ in range(args.warmup):
+            mf.run_sharded(K, sp)
+        sync_all()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            mf.run_sharded(K, sp)
+        e1.record(stream)
+        sync_all()
+        ms = e0.elapsed_time(e1) / max(args.steps, 1)
+        Cf = torch.empty((max(A.m, 1), K), device=B.device, dtype=B.dtype)
+        mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cf.data_ptr(), K, sp)
+        sync_all()
+        chk = selfcheck(A, Bh, Cf, K, npdtype)
+        out["modes"][mode] = {"bcast_B_s": round(t_b, 5),
+                              "bcast_GBs": round(bbytes * (ndist - 1) / t_b / 1e9, 1) if ndist > 1 else None,
+                              "ms_per_step": round(ms, 5), "value": round(flops / (ms * 1e-3) / 1e9, 3),
+                              "unit": "GFLOP/s", "shards": mf.ngpus()[0], "selfcheck_ok": bool(chk["ok"])}
+        mf.close()
+        del Cf
+    return out
+
+
 def dump_c(path: str, C_all, exact_all, k: int) -> None:
     """Row sample of C (every 101st row and the last row) + the exact mask of those rows (tests compare runs)."""
     import numpy as np
@@ -779,7 +850,19 @@ def main():
         except Exception as e:  # the baseline is reported, never required
             cpu = {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
     mf.close()
-    del B, C
+    del C
+
+    # ---- N>1: the in-process multi-GPU handle of the C ABI over the same matrix (rank 0; the others wait)
+    multi = None
+    if dist is not None and not args.no_multi_handle:
+        if rank == 0:
+            devs = [0] * N if args.dist_backend == "gloo" else list(range(N))
+            try:
+                multi = run_multi_handle(args, torch, S, np, p, K, npdtype, B, Bh, devs, stream)
+            except Exception as e:   # reported, the distributed line stands on its own
+                multi = {"error": f"{type(e).__name__}: {e}"}
+        dist.barrier()
+    del B
 
     dataset = None
     dataset_ok = True
@@ -821,7 +904,11 @@ def main():
             "cpu_baseline": cpu,
             "plugin_e2e": e2e,
             "dataset": dataset,
+            "multi_handle": multi,
             "setup": {"gen_s": round(t_gen, 2), "plan_s": round(t_plan, 2), "bcast_B_s": round(t_bcast, 4),
+                      "bcast_B_s_modes": None if multi is None or "modes" not in multi else
+                      {"torch.distributed rccl (one process per GPU)": round(t_bcast, 4),
+                       **{f"multi-handle {m_}": v_.get("bcast_B_s") for m_, v_ in multi["modes"].items()}},
                       "allgather_C_s": None if t_gather is None else round(t_gather, 4),
                       "selfcheck": chk, "selfcheck_all_ranks_ok": ok_all},
         }

@@ -79,8 +79,8 @@ constexpr int64_t TILE_MIN_TILES = 512;   // policy: candidate tiles (one workgr
 constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.19x on the dense band; more tiles)
 constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value -0, the zero B row)
 constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
-// Matrix-core tiles (spmm_mfma_tile_kernel): fp64, 32-column panels, rows with strictly increasing
-// columns, B below 4 GiB (32-bit buffer offsets).  Policy (measured): sampled reuse of 16-row tiles
+// Matrix-core tiles (spmm_mfma_tile_kernel): fp64 and fp32, K a multiple of 32, rows with strictly
+// increasing columns, B below 4 GiB (32-bit buffer offsets).  Policy (measured): sampled reuse of 16-row tiles
 // (nonzeros per union column; reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE, enough tiles
 // and nonzeros to fill the chip; then every 16-row tile of reuse >= MFMA_TILE_REUSE.
 constexpr double MFMA_TILE_REUSE = 2.0;     // per tile, once the matrix qualifies (panel density >= 1/8)
@@ -290,15 +290,16 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
 // Matrix-core tiles over columns [k0, k0 + kw) (kw a multiple of 32): four 16-row tiles (one per wave) per
 // workgroup; a wave owns 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (DESIGN §6.18;
 // SPMM_HIP_MFMA_NP=1 keeps 32).  B and C point at column k0; the buffer descriptor of B covers the rest of the array.
-void launch_mfma(spmm_hip_t *h, const double *B, double *C, int ld, int k0, int kw, hipStream_t s) {
+template <typename T>
+void launch_mfma(spmm_hip_t *h, const T *B, T *C, int ld, int k0, int kw, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
     const int np_max = env_int("SPMM_HIP_MFMA_NP", 2) >= 2 ? 2 : 1;
     for (int k1 = 0; k1 + 32 <= kw;) {
         const int np = (np_max >= 2 && k1 + 64 <= kw) ? 2 : 1;
-        const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)(k0 + k1)) * sizeof(double));
+        const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)(k0 + k1)) * sizeof(T));
         auto go = [&](auto xcd_c, auto np_c) {
-            spmm_mfma_tile_kernel<decltype(xcd_c)::value, decltype(np_c)::value><<<grid, WG, 0, s>>>(
-                h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const double *)h->d_tval, h->d_tlidx, B + k1, bb,
+            spmm_mfma_tile_kernel<T, decltype(xcd_c)::value, decltype(np_c)::value><<<grid, WG, 0, s>>>(
+                h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const T *)h->d_tval, h->d_tlidx, B + k1, bb,
                 C + k1, ld);
         };
         using N1 = std::integral_constant<int, 1>;
@@ -315,9 +316,7 @@ template <typename T>
 void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStream_t rs) {
     T *P = (T *)h->d_part;
     // matrix-core tiles: one pass over all K columns (the row kernel's K panels are for its B gather, not theirs)
-    if constexpr (std::is_same_v<T, double>) {
-        if (h->plan.ntile > 0 && h->plan.tile_mfma) launch_mfma(h, B, C, K, 0, K, s);
-    }
+    if (h->plan.ntile > 0 && h->plan.tile_mfma) launch_mfma<T>(h, B, C, K, 0, K, s);
     for (int p = 0; p < h->plan.npanels; ++p) {
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
@@ -1141,8 +1140,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         // policy's per-tile threshold (what the policy runs once a matrix qualifies; A/B measurements)
         const int env_m = env_int("SPMM_HIP_MFMA", 0);
         const int fm = h->var.mfma != 0 ? h->var.mfma : env_m;
-        const bool mshape = fm >= 0 && h->vsize == 8 && k % 32 == 0 &&
-                            (double)h->ncols * (double)k * 8.0 < 4294967296.0;
+        const bool mshape = fm >= 0 && k % 32 == 0 && (double)h->ncols * (double)k * (double)h->vsize < 4294967296.0;
         if (forced >= 0 && h->nnz > 0 && h->ncols < INT32_MAX && win_forced <= 0 && (mshape || shape_ok)) {
             if (int st = load_cols()) return st;
             if (mshape && (gate_only || rows_strict(h->h_row_ptr.data(), hcol, h->m))) {

@@ -3,7 +3,8 @@
 // The sparse tile kernel (spmm_kernels.hpp, spmm_tile_kernel) reads one staged B row from LDS per nonzero and does
 // VEC FMAs with it: the dense-row classes of the medium dataset sit at ~4 useful FMAs/clk/CU, bound by the LDS /
 // L2 operand path.  Here every chunk of a tile is multiplied as a DENSE panel on the matrix
-// cores,   C_tile[16 x 32 NP] += A_panel[16 x U] . B_chunk[U x 32 NP]   with v_mfma_f64_16x16x4_f64:
+// cores,   C_tile[16 x 32 NP] += A_panel[16 x U] . B_chunk[U x 32 NP]   with v_mfma_f64_16x16x4_f64 (fp64) or
+// v_mfma_f32_16x16x4_f32 (fp32):
 //   * a tile is 16 consecutive rows and belongs to ONE wave (four independent tiles per workgroup, no barrier);
 //   * A_panel: the chunk's nonzeros scattered into the wave's zeroed LDS panel (row x chunk-local union column);
 //     LDS operations of one wave execute in order, so the wave clears and refills its own panel without a barrier;
@@ -15,26 +16,29 @@
 //   * one MFMA does 1,024 FMAs from one f64 of A and one of B per lane (~16x less operand traffic per FMA than the
 //     sparse kernel); the zero padding of the panel costs MFMA issue instead (useful fraction = panel density).
 //
-// Exactness.  The f64 MFMA accumulates its four products into C in k order, each one fused multiply-add (measured
-// bit for bit against the reference chain, tests/test_gpu_mfma.py), so a tile row is the reference's left-to-right
+// Exactness.  Both MFMAs accumulate their four products into C in k order, each one fused multiply-add (measured
+// bit for bit, tools/mfma_chain_probe.py: 25,600 of 25,600 outputs each; and against the reference chain,
+// tests/test_gpu_mfma.py), so a tile row is the reference's left-to-right
 // chain over its own columns with extra fma(0, b, acc) steps for the panel's empty cells.  Those extra steps are
 // exact no-ops -- and the result does not depend on how the matrix cores treat subnormals -- whenever every nonzero
-// operand the tile's MFMAs see (panel values a, B operand values b) has 2^-458 <= |x| <= 2^500:
+// operand the tile's MFMAs see (panel values a, B operand values b) has |x| >= 2^-458 (fp32: 2^-40, the same
+// argument with 24-bit significands and a 2^-126 normal floor) and the chain stays finite (fp64 figures below):
 //   * the chain starts at +0; a product is then 0 (an empty cell or a zero value: acc + (+-0) == acc, and +0 stays
 //     +0) or at least 2^-916 in magnitude with its last bit >= 2^-1020; a step a*b + acc either cancels exactly
 //     (+0, as in the reference) or lands at >= 2^-1021 in magnitude (|acc| near |a*b| has its last bit >= 2^-969,
-//     otherwise one term dominates) -- so no step underflows, none produces -0 or a subnormal, none overflows
-//     (<= 2048 products of <= 2^1000), and an empty cell never meets a -0 accumulator (fma(+0, b, -0) would give
-//     +0 where the reference keeps -0).
-// The check is made on the operands as they enter the MFMAs (no extra registers live); a wave that meets an operand
-// outside the range -- Inf/NaN in B, subnormal or extreme values: adversarial data only -- recomputes its whole tile
-// by the sparse chain over the real entries with IEEE FMAs (exactly the reference's operations), from +0.  Rows with
-// a repeated column (duplicate .mtx entries) never reach this kernel (the inspector keeps them out).
+//     otherwise one term dominates) -- so no step underflows or produces a subnormal, no -0 ever appears, and an
+//     empty cell never meets a -0 accumulator (fma(+0, b, -0) would give +0 where the reference keeps -0);
+//   * Inf / NaN in B (a panel zero times it makes a NaN the reference does not have) and overflow leave a
+//     non-finite accumulator, which stays non-finite to the chunk's end.
+// A wave checks both after every chunk (the smallest frexp exponent it fed to the MFMAs, the finiteness of its
+// accumulators); on a failure -- adversarial data only -- it recomputes its whole tile by the sparse chain over the
+// real entries with IEEE FMAs (exactly the reference's operations), from +0.  Rows with a repeated column
+// (duplicate .mtx entries) never reach this kernel (the inspector keeps them out).
 //
 // Per-wave pipeline, chunk c: A(c) from the panel into VGPRs; clear chunk c's cells, scatter chunk c+1's entries
 // (loaded during chunk c-1); issue the entry loads of chunk c+2; the MFMAs of chunk c (operands range-checked), each
 // k step's B registers reloaded with chunk c+1's operand as soon as its MFMAs have issued; the union-column loads of
-// chunk c+2.  VGPRs: 154 (NP = 1, 3 waves per SIMD) / 218 (NP = 2, 2 waves per SIMD), no spills.
+// chunk c+2; the exact-range ballot.
 //
 // Tables (inspector build_tiles with 16-row tiles; spmm_engine.hip):
 //   tiles[t]   = {first C row, rows (<= 16), first chunk, chunks}
@@ -58,40 +62,67 @@ constexpr int MFMA_PSZ = MFMA_TRASH + 2;       // one wave's panel (+ trash cell
 constexpr int MFMA_CAPA = 512;                 // entries per chunk (8 per lane)
 constexpr int MFMA_NPE = MFMA_CAPA / 64;
 
-// operand outside the exact-chain range (see the header): nonzero and |x| < 2^-458, |x| > 2^500, Inf or NaN
-__device__ __forceinline__ bool mfma_operand_bad(double x) {
-    const double ax = __builtin_fabs(x);
-    return !(ax >= 0x1p-458 && ax <= 0x1p500) && x != 0.0;
-}
-template <bool XCD, int NP>
-__global__ __launch_bounds__(256, NP == 1 ? 3 : 2) void spmm_mfma_tile_kernel(const int4 *__restrict__ tiles,
-                                                                              int ntiles,
-                                                                              const int4 *__restrict__ tchunk,
-                                                                              const int32_t *__restrict__ tcolT,
-                                                                              const double *__restrict__ tval,
-                                                                              const uint16_t *__restrict__ tpos,
-                                                                              const double *__restrict__ B,
-                                                                              uint32_t b_bytes, double *__restrict__ C,
-                                                                              int ld) {
-    __shared__ __attribute__((aligned(16))) double spanel[4 * MFMA_PSZ];
+// Per value type: the 16x16x4 MFMA, its accumulator, the B operand piece a lane loads (columns 2j, 2j+1 of a
+// 32-column sub-panel: 16 B fp64 / 8 B fp32), the C/D row map (f64: row = g + 4i; f32: row = 4g + i, g = lane >> 4 --
+// measured, tools/mfma_chain_probe.py) and the exactness range (see the header): a nonzero operand needs a frexp
+// exponent >= MIN_EXP, |x| >= 2^-458 fp64 / 2^-40 fp32 (zero has exponent 0, a subnormal far less).  The kernel
+// keeps the smallest exponent a lane has fed to its MFMAs (one v_frexp_exp + one v_min per operand).
+template <typename T> struct MfmaT;
+template <> struct MfmaT<double> {
+    typedef f64x4 acc_t;
+    typedef i32x4 bop_t;
+    static constexpr int MIN_EXP = -457;
+    __device__ static int fexp(double x) { return __builtin_amdgcn_frexp_exp(x); }
+    __device__ static acc_t mfma(double a, double b, acc_t c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+    __device__ static bop_t load(__amdgpu_buffer_rsrc_t rs, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0); }
+    __device__ static int row(int g, int i) { return g + 4 * i; }
+    __device__ static bool owns(int r, int g) { return (r & 3) == g; }
+    __device__ static int slot(int r) { return r >> 2; }
+    __device__ static double fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+};
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+template <> struct MfmaT<float> {
+    typedef f32x4 acc_t;
+    typedef i32x2 bop_t;
+    static constexpr int MIN_EXP = -39;
+    __device__ static int fexp(float x) { return __builtin_amdgcn_frexp_expf(x); }
+    __device__ static acc_t mfma(float a, float b, acc_t c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+    __device__ static bop_t load(__amdgpu_buffer_rsrc_t rs, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0); }
+    __device__ static int row(int g, int i) { return 4 * g + i; }
+    __device__ static bool owns(int r, int g) { return (r >> 2) == g; }
+    __device__ static int slot(int r) { return r & 3; }
+    __device__ static float fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+};
+
+template <typename T, bool XCD, int NP>
+__global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm_mfma_tile_kernel(
+    const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
+    const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, uint32_t b_bytes,
+    T *__restrict__ C, int ld) {
+    using M = MfmaT<T>;
+    typedef typename M::acc_t acc_t;
+    typedef typename M::bop_t bop_t;
+    constexpr uint32_t SUB = 32u * sizeof(T);   // bytes of one 32-column sub-panel of a B row
+    __shared__ __attribute__((aligned(16))) T spanel[4 * MFMA_PSZ];
     const int wave = threadIdx.x / 64, l = threadIdx.x % 64;
     const int wg = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int t = __builtin_amdgcn_readfirstlane(wg * 4 + wave);
     if (t >= ntiles) return;
     const int4 tl = tiles[t];
-    double *P = spanel + wave * MFMA_PSZ;
-    for (int i = l; i < MFMA_PSZ; i += 64) P[i] = 0.0;
+    T *P = spanel + wave * MFMA_PSZ;
+    for (int i = l; i < MFMA_PSZ; i += 64) P[i] = T(0);
 
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)B, (short)0, (int)b_bytes, 0x00020000);
-    const uint32_t ldb = (uint32_t)ld * 8u, lane_off = (uint32_t)(l & 15) * 16u;
+    const uint32_t ldb = (uint32_t)ld * (uint32_t)sizeof(T), lane_off = (uint32_t)(l & 15) * 2u * (uint32_t)sizeof(T);
     const int g = l >> 4;
 
-    f64x4 acc[NP][2];
+    acc_t acc[NP][2];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = f64x4{0.0, 0.0, 0.0, 0.0};
-    i32x4 bo[NP][MFMA_KS];
+    for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = acc_t{T(0), T(0), T(0), T(0)};
+    bop_t bo[NP][MFMA_KS];
     int tcn[MFMA_KS];
-    double ev[MFMA_NPE];
+    T ev[MFMA_NPE];
     int ep[MFMA_NPE], hc[MFMA_NPE];
     int ne = 0;
     auto load_tcol = [&](int c) {                 // this lane's 12 union columns of chunk c (3 x 16 B)
@@ -104,8 +135,7 @@ __global__ __launch_bounds__(256, NP == 1 ? 3 : 2) void spmm_mfma_tile_kernel(co
     };
     auto load_b1 = [&](int st) {
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
-            bo[p][st] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)tcn[st] * ldb + lane_off + 256u * p, 0, 0);
+        for (int p = 0; p < NP; ++p) bo[p][st] = M::load(rs, (uint32_t)tcn[st] * ldb + lane_off + SUB * p);
     };
     auto load_e = [&](int c) {
         const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
@@ -126,11 +156,11 @@ __global__ __launch_bounds__(256, NP == 1 ? 3 : 2) void spmm_mfma_tile_kernel(co
         }
     };
     // chunk c by the sparse chain (IEEE FMAs over the chunk's real entries in order, from the accumulators): an
-    // entry of row r updates this lane's outputs when r % 4 == g (the fallback of a tile with an operand outside the
-    // exact range)
+    // entry of row r updates this lane's outputs when the lane owns row r (the fallback of a tile with an operand
+    // outside the exact range)
     auto sparse_chunk = [&](int c) {
         const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
-        double x[NP][8];
+        T x[NP][8];
 #pragma unroll
         for (int p = 0; p < NP; ++p)
 #pragma unroll
@@ -139,19 +169,19 @@ __global__ __launch_bounds__(256, NP == 1 ? 3 : 2) void spmm_mfma_tile_kernel(co
         for (int e = ch.z; e < cn.z; ++e) {
             const int cell = (int)tpos[e];
             const int r = cell / MFMA_PST, k = cell % MFMA_PST;
-            if (cell == MFMA_TRASH || (r & 3) != g) continue;
+            if (cell == MFMA_TRASH || !M::owns(r, g)) continue;
             const int row = tcolT[(size_t)(tl.z + c) * MFMA_UC + (k & 3) * MFMA_KS + (k >> 2)];
-            const double av = tval[e];
+            const T av = tval[e];
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-                const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)row * ldb + lane_off + 256u * p, 0, 0);
-                double bb[2];
-                __builtin_memcpy(bb, &v, 16);
+                const bop_t v = M::load(rs, (uint32_t)row * ldb + lane_off + SUB * p);
+                T bb[2];
+                __builtin_memcpy(bb, &v, 2 * sizeof(T));
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if (q == (r >> 2)) {
-                        x[p][q] = __builtin_fma(av, bb[0], x[p][q]);
-                        x[p][4 + q] = __builtin_fma(av, bb[1], x[p][4 + q]);
+                    if (q == M::slot(r)) {
+                        x[p][q] = M::fma(av, bb[0], x[p][q]);
+                        x[p][4 + q] = M::fma(av, bb[1], x[p][4 + q]);
                     }
             }
         }
@@ -169,46 +199,54 @@ __global__ __launch_bounds__(256, NP == 1 ? 3 : 2) void spmm_mfma_tile_kernel(co
     scatter();
     load_e(min(1, tl.w - 1));
     load_tcol(min(1, tl.w - 1));
+    int emin = 0;          // smallest frexp exponent of an operand this lane fed to the MFMAs
     bool bad = false;
     for (int c = 0; c < tl.w; ++c) {
         const int ns = (tchunk[tl.z + c].y + 3) >> 2;
-        double a[MFMA_KS];
-        const double *pa = P + (l & 15) * MFMA_PST + g;
+        T a[MFMA_KS];
+        const T *pa = P + (l & 15) * MFMA_PST + g;
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
 #pragma unroll
-        for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = 0.0;
+        for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
         if (c + 1 < tl.w) scatter();
         load_e(min(c + 2, tl.w - 1));
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) {
             if (st < ns) {
-                bad |= mfma_operand_bad(a[st]);
+                emin = min(emin, M::fexp(a[st]));
 #pragma unroll
                 for (int p = 0; p < NP; ++p) {
-                    double bb[2];
-                    __builtin_memcpy(bb, &bo[p][st], 16);
-                    bad |= mfma_operand_bad(bb[0]) || mfma_operand_bad(bb[1]);
-                    acc[p][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[0], acc[p][0], 0, 0, 0);
-                    acc[p][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st], bb[1], acc[p][1], 0, 0, 0);
+                    T bb[2];
+                    __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
+                    emin = min(emin, min(M::fexp(bb[0]), M::fexp(bb[1])));
+                    acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
+                    acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
                 }
             }
             load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
         }
+        // an operand below the range, or a non-finite accumulator (Inf/NaN in B -- a panel zero times it is NaN --,
+        // or an overflow): the tile goes to the sparse chain
+        bad = emin < M::MIN_EXP;
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bad |= !__builtin_isfinite(acc[p][0][i]) || !__builtin_isfinite(acc[p][1][i]);
         if (__builtin_amdgcn_ballot_w64(bad)) break;
         load_tcol(min(c + 2, tl.w - 1));
     }
-    if (__builtin_amdgcn_ballot_w64(bad)) {      // an operand outside the exact range: the tile by the sparse chain
+    if (__builtin_amdgcn_ballot_w64(bad)) {      // outside the exact range: the whole tile by the sparse chain
 #pragma unroll
-        for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = f64x4{0.0, 0.0, 0.0, 0.0};
+        for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = acc_t{T(0), T(0), T(0), T(0)};
         for (int c = 0; c < tl.w; ++c) sparse_chunk(c);
     }
     const int c0 = 2 * (l & 15);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int r = g + 4 * i;
+        const int r = M::row(g, i);
         if (r < tl.y) {
-            double *p = C + (size_t)(tl.x + r) * ld + c0;
+            T *p = C + (size_t)(tl.x + r) * ld + c0;
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 __builtin_nontemporal_store(acc[q][0][i], p + 32 * q);

@@ -66,7 +66,7 @@ def test_debug_plan_forced_modes(S):
     assert S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, mfma=1)["mode"] == "mfma"
     assert S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, mfma=-1)["mode"] != "mfma"
     f32 = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, dtype=S.F32, mfma=1)
-    assert f32["mode"] != "mfma"                         # fp32 never takes the f64 matrix-core tiles
+    assert f32["mode"] == "mfma"                         # fp32 matrix-core tiles (v_mfma_f32_16x16x4_f32)
     assert S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 8, mfma=1)["mode"] != "mfma"   # K not a multiple of 32
 
 

@@ -4,6 +4,8 @@
   strong split of config 2 by the reference partitioner (lib/parallel_util.h:141-165), B broadcast, per-rank HIP-event
   timing (value from the slowest rank), C all-gathered once, every rank self-checked.  The gathered C must
   be bit-equal to the one-rank run on every sampled row both runs compute exactly.
+  The same run drives the in-process multi-GPU handle of the C ABI (spmm_hip_create_multi, shards on repeated
+  device 0): peer B broadcast, spmm_hip_run_sharded timed, C gathered and self-checked.
 * `--workload medium-sample` on a small stride: the dataset record's fields (aggregate, fractions, CPU baseline).
 """
 import json
@@ -42,6 +44,14 @@ def test_bench_two_ranks_share_one_gpu(tmp_path):
     assert abs(two["value"] - 2 * two["config"]["nnz_total"] * 32 / (two["ms_per_step"] * 1e-3) / 1e9) < 1e-3 * two["value"]
     assert two["wall_ms_per_step"] >= 0.9 * two["ms_per_step"]
     assert two["setup"]["allgather_C_s"] is not None and two["dataset"] is None
+    # the in-process multi-GPU handle (spmm_hip_create_multi) on repeated devices: peer broadcast, sharded runs
+    mh = two["multi_handle"]
+    assert mh is not None and "error" not in mh, mh
+    assert mh["devices"] == [0, 0] and mh["nnz"] == two["config"]["nnz_total"]
+    peer = mh["modes"]["peer"]
+    assert peer["shards"] == 2 and peer["selfcheck_ok"] is True and peer["bcast_B_s"] > 0 and peer["value"] > 0
+    assert "skipped" in mh["modes"]["rccl"]                  # RCCL needs distinct devices
+    assert two["setup"]["bcast_B_s_modes"]["multi-handle peer"] == peer["bcast_B_s"]
     one = _bench(["--workload", "config2", "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-dataset",
                   "--dump-c", str(c1)])
     assert one["n_gpus"] == 1 and one["setup"]["selfcheck_all_ranks_ok"] is True

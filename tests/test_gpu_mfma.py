@@ -95,10 +95,10 @@ def test_mfma_nonfinite_b(env, monkeypatch):
 
 
 def test_mfma_refused(env, monkeypatch):
-    """fp32, 8-column panels and repeated columns never take matrix-core tiles (another kernel runs, still exact)."""
+    """K not a multiple of 32 and repeated columns never take matrix-core tiles (another kernel runs, still exact)."""
     torch, S, O = env
     A = S.generate(S.gen_params(MATS[1]))
-    for vals, k in ((A.values.astype(np.float32), 32), (A.values, 8)):
+    for vals, k in ((A.values.astype(np.float32), 48), (A.values, 8)):
         mf = handle(S, A, vals, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
         assert mf.tile_info()["mode"] != "mfma"
         mf.close()
@@ -317,3 +317,55 @@ def test_debug_plan_matches_handle(env, monkeypatch):
             assert d["mode"] == ti["mode"] and d["ntile"] == ti["tiles"] and d["tile_nnz"] == ti["nnz"]
             assert d["seq_max"] == inf[8] and d["blocks"] == inf[5] and d["exact_rows"] == inf[17]
             mf.close()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# fp32 matrix-core tiles: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain (tools/mfma_chain_probe.py,
+# profiles/r04/chain_probe.jsonl), so fp32 tile rows equal the reference FLOAT build's chain (the oracle's fp32 path is
+# pinned to it, tests/test_oracle_golden.py) bit for bit.
+
+@pytest.mark.parametrize("line", MATS, ids=["similar", "dense", "split", "lowreuse"])
+@pytest.mark.parametrize("k", [32, 64, 128])
+def test_mfma_f32_bitexact(env, monkeypatch, line, k):
+    torch, S, O = env
+    A = S.generate(S.gen_params(line))
+    vals = (A.values * np.where(np.arange(A.nnz) % 3 == 0, -1.0, 1.0)).astype(np.float32)
+    x = (O.drand48(17 + k, A.ncols * k) * 2.0 - 1.0).astype(np.float32)
+    y1, t1, ex1 = run(S, A, vals, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    assert t1["mode"] == "mfma" and t1["tiles"] > 0
+    y0, t0, ex0 = run(S, A, vals, x, k, monkeypatch, {"SPMM_HIP_TILES": "-1"})
+    both = ex0 & ex1
+    assert both.sum() >= t1["rows"] * 0.99
+    assert np.array_equal(bits(y1[both]), bits(y0[both]))
+    seq = O.spmm(A.row_ptr, A.col_idx, vals, A.ncols, x, k)
+    assert np.array_equal(bits(y1[ex1]), bits(seq[ex1]))
+
+
+def edge_values_f32(kind, n, rng):
+    na, nb = n
+    sa, sb = rng.choice([-1.0, 1.0], na), rng.choice([-1.0, 1.0], nb)
+    ua, ub = rng.uniform(0.5, 1.5, na), rng.uniform(0.5, 1.5, nb)
+    if kind == "subnormal":          # f32 subnormals (2^-149 .. 2^-127) against values up to 2^30
+        a, b = sa * ua * 2.0 ** rng.integers(-145, -128, na), sb * ub * 2.0 ** rng.integers(0, 30, nb)
+    elif kind == "underflow":        # products 2^-150 .. 2^-110: subnormal sums, underflow to +-0
+        a, b = sa * ua * 2.0 ** rng.integers(-75, -55, na), sb * ub * 2.0 ** rng.integers(-75, -55, nb)
+    elif kind == "near_range":       # around the fp32 bound 2^-40
+        a, b = sa * 2.0 ** rng.choice([-41, -40, -39, 0, 60], na), sb * 2.0 ** rng.choice([-41, -40, 0, 1], nb)
+    elif kind == "overflow":
+        a, b = sa * ua * 2.0 ** rng.integers(60, 70, na), sb * ub * 2.0 ** rng.integers(60, 70, nb)
+    else:
+        raise ValueError(kind)
+    return a.astype(np.float32), b.astype(np.float32)
+
+
+@pytest.mark.parametrize("kind", ["subnormal", "underflow", "near_range", "overflow"])
+def test_mfma_f32_edge_values(env, monkeypatch, kind):
+    torch, S, O = env
+    A = S.generate(S.gen_params(MATS[0]))
+    k = 32
+    rng = np.random.default_rng(zlib.crc32(f"f32/{kind}".encode()))
+    vals, x = edge_values_f32(kind, (A.nnz, A.ncols * k), rng)
+    y, t, ex = run(S, A, vals, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    assert t["mode"] == "mfma"
+    want = O.spmm(A.row_ptr, A.col_idx, vals, A.ncols, x, k)
+    assert same_bits_or_nan(y[ex], want[ex]), kind

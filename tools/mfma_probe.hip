@@ -22,8 +22,8 @@ extern "C" int mfma_probe_launch(int ntiles, const void *tiles, const void *tchu
     auto c = (double *)C;
     if (b_bytes >= (1ll << 32)) return -2;
     if (xcd & 1)
-        spmm_mfma_tile_kernel<true><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
+        spmm_mfma_tile_kernel<true, 1><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
     else
-        spmm_mfma_tile_kernel<false><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
+        spmm_mfma_tile_kernel<false, 1><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes, c, ld);
     return (int)hipGetLastError();
 }

@@ -151,6 +151,25 @@ def cpu_baseline(O, A, vals, x_col, k, budget_s, cores):
             "cpu_cores": cores}
 
 
+class env_set:
+    """Set ENV=V,ENV=V for the duration of a with-block (the engine reads its policy overrides at plan time)."""
+    def __init__(self, spec):
+        self.kv = dict(x.split("=", 1) for x in (spec or "").split(",") if x)
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def spawn_workers(args) -> int:
     """Run --workers copies of this sweep over interleaved slices of the work list, one output file each
     (<out stem>.w<i>.jsonl: tools/sweep_merge.py folds them), sharing one GPU lock; exit with the worst status."""
@@ -198,6 +217,14 @@ def main():
     ap.add_argument("--workers", type=int, default=1, help="host worker processes (timed regions serialised)")
     ap.add_argument("--worker", default=None, help=argparse.SUPPRESS)     # i/W: set by --workers
     ap.add_argument("--gpu-lock", default=None, help="lock file serialising the timed regions of the workers")
+    ap.add_argument("--env", default="", help="ENV=V,ENV=V set while the engine plans (e.g. SPMM_HIP_MFMA=2)")
+    ap.add_argument("--base-env", default=None,
+                    help="A/B: also plan a baseline handle with these ENV=V,... (e.g. SPMM_HIP_MFMA=-1: the plan without "
+                         "matrix-core tiles) and time both interleaved in the same process; exact rows of both must agree "
+                         "bit for bit")
+    ap.add_argument("--census", default=None,
+                    help="keep only the (line, K) pairs whose census record (tools/plan_census.py) has mode == --census-mode")
+    ap.add_argument("--census-mode", default="mfma")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "sweep.jsonl"))
     args = ap.parse_args()
     if args.workers > 1 and args.worker is None:
@@ -236,11 +263,19 @@ def main():
     # (dataset index, line) still to do; matrices are generated one ahead on a host thread (the generator and the
     # feature extractor release the GIL), so the GPU does not wait on the host between matrices
     idx_lines = dataset_index_lines(args)
+    census = None
+    if args.census:
+        census = set()
+        for l in open(args.census):
+            d = json.loads(l)
+            if d.get("mode") == args.census_mode:
+                census.add((d["gen"], int(d["k"])))
     work = []
     for idx, line in idx_lines:
         if idx in done_idx:
             continue
-        todo = [(dt, k) for dt in dtypes for k in ks if (line, k, dt) not in done]
+        todo = [(dt, k) for dt in dtypes for k in ks if (line, k, dt) not in done
+                and (census is None or (line, k) in census)]
         if not todo:
             continue
         p = S.gen_params(line)
@@ -291,32 +326,48 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
         vals = A.values.astype(dtype)
         tc = time.time()
         mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
+        mfb = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0) if args.base_env is not None else None
         t_create = time.time() - tc
         for dt2, k in todo:
             if dt2 != dt:
                 continue
             t0 = time.time()
-            mf.plan(k)
+            with env_set(args.env):
+                mf.plan(k)
             t_plan = time.time() - t0
+            if mfb is not None:
+                with env_set(args.base_env):
+                    mfb.plan(k)
             g = torch.Generator(device=dev)
             g.manual_seed(42)
             B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
             Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
             run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
+            Cb = runb = None
+            if mfb is not None:
+                Cb = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
+                runb = lambda: mfb.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cb.data_ptr(), k, stream.cuda_stream)  # noqa
             torch.cuda.synchronize()
             if lock_f:
                 fcntl.flock(lock_f, fcntl.LOCK_EX)
-            for _ in range(args.warmup):
-                run()
-            ms_b = []
-            for _ in range(args.batches):
+
+            def timed(fn):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(args.iters):
-                    run()
+                    fn()
                 e1.record(stream)
                 torch.cuda.synchronize()
-                ms_b.append(e0.elapsed_time(e1) / args.iters)
+                return e0.elapsed_time(e1) / args.iters
+            for _ in range(args.warmup):
+                run()
+                if runb is not None:
+                    runb()
+            ms_b, msb_b = [], []
+            for _ in range(args.batches):          # baseline and policy interleaved batch by batch
+                if runb is not None:
+                    msb_b.append(timed(runb))
+                ms_b.append(timed(run))
             if lock_f:
                 fcntl.flock(lock_f, fcntl.LOCK_UN)
             ms = min(ms_b)
@@ -336,6 +387,20 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
                    "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
                               "timed": round(t_timed, 3), "check": round(t_check, 3)},
                    **par}
+            if mfb is not None:
+                exb = mfb.exact_rows() & mf.exact_rows()
+                ext = torch.from_numpy(exb).to(dev)
+                it = torch.int64 if dt == "f64" else torch.int32
+                rec.update({"ms_base": min(msb_b), "batches_base": [round(x, 5) for x in msb_b],
+                            "speedup": min(msb_b) / ms, "base_env": args.base_env,
+                            "tile_mode_base": mfb.tile_info()["mode"],
+                            "bitexact_vs_base": bool(torch.equal(Cm[ext].view(it), Cb[ext].view(it)))})
+            if args.env:
+                rec["env"] = args.env
+            if rec["tile_mode"] != "none":
+                ti = mf.tile_info()
+                rec.update({"tile_rows": ti["rows"], "tile_nnz": ti["nnz"], "tile_chunks": ti["chunks"],
+                            "tile_reuse": ti["reuse"]})
             if feat is not None:
                 rec["mem_mb"] = feat["mem_footprint"]
                 rec["features"] = {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled",
@@ -347,10 +412,12 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
             with open(out, "a") as f:
                 f.write(json.dumps(rec) + "\n")
             print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
-                                                         "roofline_frac", "cpu_gflops", "bitexact_seq_rows",
+                                                         "roofline_frac", "cpu_gflops", "speedup", "bitexact_seq_rows",
                                                          "normwise_ok")}), flush=True)
-            del B, Cm
+            del B, Cm, Cb
         mf.close()
+        if mfb is not None:
+            mfb.close()
 
 
 if __name__ == "__main__":
