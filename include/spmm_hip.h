@@ -262,10 +262,16 @@ void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t);
  * [10] split length T, [11] piece length of rows > T, [12] K-panel width, [13] K panels, [14] tiles built,
  * [15] nonzeros in tiles, [16] chunks, [17] row-kernel blocks, [18] split rows, [19] exact rows, [20] vector lanes,
  * [21] XCD order, [22] column windows, [23] 1 = gate only, [24]/[25] plan fingerprint (low / high 32 bits; two
- * plans are the same exactly when these agree). */
+ * plans are the same exactly when these agree), [26] est. taken tiles. */
 #define SPMM_HIP_PLAN_SLOTS 32
 int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t k,
                         int32_t dtype, int32_t mfma, int32_t gate_only, double *out);
+/* Diagnostics (host only): the matrix-core gate's cost model on a recorded sample -- sample[7] =
+ * {tiles sampled, mean reuse, fraction taken, est. taken tiles, est. nonzeros in them, est. chunks, largest sampled
+ * chunk count} as spmm_hip_debug_plan reports them ([9], [2], [3], [26], [4], [5], [6]); out[3] = {verdict, model
+ * time with matrix-core tiles (us), without (us)}.  Lets a census re-decide with this library's constants without
+ * regenerating the matrices (tools/plan_census.py --regate). */
+int spmm_hip_debug_gate(int64_t nnz, int32_t k, const double *sample, double *out);
 
 const char *spmm_hip_strerror(int status);
 const char *spmm_hip_last_error_detail(void);

@@ -80,15 +80,13 @@ constexpr int TILE_ROWS = 32;             // rows per tile (32: 1.22x vs 64: 1.1
 constexpr int TILE_SEG_ALIGN = 4;         // row segments padded to this many entries (value -0, the zero B row)
 constexpr uint16_t TILE_PAD_LIDX = 0xFFFF;   // chunk-local column of a padding entry
 // Matrix-core tiles (spmm_mfma_tile_kernel): fp64 and fp32, K a multiple of 32, rows with strictly
-// increasing columns, B below 4 GiB (32-bit buffer offsets).  Policy (measured): sampled reuse of 16-row tiles
-// (nonzeros per union column; reuse / 16 = the panel density the MFMAs see) at least MFMA_MIN_REUSE, enough tiles
-// and nonzeros to fill the chip; then every 16-row tile of reuse >= MFMA_TILE_REUSE.
-constexpr double MFMA_TILE_REUSE = 2.0;     // per tile, once the matrix qualifies (panel density >= 1/8)
+// increasing columns, B below 4 GiB (32-bit buffer offsets).  Policy (the cost-model gate, mfma_sample / mfma_cost,
+// DESIGN §6.18): 16-row tiles with enough nonzeros per chunk, taken when the model's time beats the row kernel's.
+constexpr double MFMA_TILE_REUSE = 2.0;     // per tile: reuse (nonzeros per union column) floor, and MFMA_TILE_NPC
 // Leftover rows of a plan whose tiles hold more than 1 - GAP_SHORT_FRAC of the nonzeros run as pieces of at most
 // GAP_SEQ_MAX nonzeros (a lone long row would otherwise be a serial straggler after the tile kernel).
 constexpr double GAP_SHORT_FRAC = 0.125;
 constexpr int GAP_SEQ_MAX = 64;
-constexpr int64_t MFMA_MIN_TILES = 1024;
 
 int pow2_ceil(int64_t x) {
     int p = 1;
@@ -828,7 +826,8 @@ double tile_reuse(const int32_t *rp, const int32_t *col, int64_t r0, int64_t r1,
 // list (<= colmax) and it makes <= dmax chunks -- a candidate over the last two is halved until it fits.  Rows must
 // be sorted (checked by the caller).  Returns false when no tile qualifies.
 bool build_tiles(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, int rmax, int uc, int capa,
-                 double min_reuse, TilePlan &tp, int colmax = INT32_MAX, int dmax = INT32_MAX) {
+                 double min_reuse, TilePlan &tp, int colmax = INT32_MAX, int dmax = INT32_MAX,
+                 double min_npc = 0.0) {
     tp = TilePlan();
     tp.in_tile.assign((size_t)m, 0);
     std::vector<int32_t> stamp((size_t)ncols, -1), pos((size_t)ncols, 0);
@@ -873,6 +872,9 @@ bool build_tiles(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols
             u0 = u1;
         }
         if ((int64_t)cut.size() - 1 > dmax) return SHRINK;
+        // matrix-core tiles: a tile must bring enough nonzeros per chunk (per dense panel product) to beat the row
+        // kernel on its rows (mfma_cost); otherwise its rows stay with the row kernel
+        if ((double)nnz < min_npc * (double)(cut.size() - 1)) return SKIP;
         const int c_first = (int)tp.chunks.size();
         std::vector<int32_t> rowp(rp + r, rp + r1);     // per row: next nonzero not yet placed
         for (size_t ci = 0; ci + 1 < cut.size(); ++ci) {
@@ -966,24 +968,46 @@ double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64
 // (reuse >= MFMA_TILE_REUSE) scaled to the matrix give the work of the tile kernel and of the row kernel on the same
 // rows, priced by mfma_cost (measured constants).
 constexpr int MFMA_GATE_SAMPLE = 256;
+// The tile kernel's cost model (us; fitted on same-process A/B data, tools/fit_mfma_gate.py).  Per
+// 32-column sub-panel the tile kernel streams each chunk's B rows and MFMAs at a chip-wide rate (MFMA_US_CHUNK per
+// chunk, MFMA_US_TILE per tile for its prologue / epilogue) unless it has too few tiles to fill the chip, when the
+// longest tiles' chunk chains bound it (MFMA_US_CHAIN per chunk); the row kernel gathers one B row per nonzero per
+// sub-panel (ROW_US_NNZ).  A tile is worth a dense panel product when its nonzeros per chunk reach
+// MFMA_TILE_NPC; a matrix takes matrix-core tiles when the model's time with them (tiles beside the leftover rows)
+// beats the row kernel's by MFMA_MIN_GAIN.
+constexpr double MFMA_US_CHUNK = 1.55e-3;
+constexpr double MFMA_US_TILE = 2.0e-3;
+constexpr double MFMA_US_CHAIN = 4.5;
+constexpr double MFMA_US_LAUNCH = 6.0;
+constexpr double ROW_US_NNZ = 12.0e-6;
+constexpr double MFMA_TILE_NPC = 150.0;     // nonzeros per chunk for a tile to be taken
+constexpr double MFMA_MIN_GAIN = 1.10;      // predicted t_off / t_on
+constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
 struct MfmaGate {
     int sampled = 0;          // candidate tiles sampled (all rows <= T, not empty)
     double r16 = 0.0;         // mean reuse of the sampled tiles (nonzeros per union column)
-    double take = 0.0;        // fraction of sampled tiles the build would take (reuse >= MFMA_TILE_REUSE)
+    double take = 0.0;        // fraction of sampled tiles the build would take
+    double tiles = 0.0;       // estimated taken tiles (whole matrix)
     double tile_nnz = 0.0;    // estimated nonzeros in taken tiles (whole matrix)
     double chunks = 0.0;      // estimated chunks of the taken tiles (whole matrix)
     double max_chunks = 0.0;  // largest chunk count of a sampled taken tile
-    double t_on = 0.0, t_off = 0.0;   // cost model (us): tiles + leftover rows vs the row kernel alone
+    double t_on = 0.0, t_off = 0.0;   // cost model (us): tiles beside the leftover rows vs the row kernel alone
     int verdict = 0;          // 1 = matrix-core tiles
 };
 
-MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T) {
+// chunks build_tiles cuts for a tile of nnz entries over nu union columns: <= MFMA_UC columns and <= room entries
+inline double mfma_chunks_est(double nnz, double nu) {
+    const double room = MFMA_CAPA - (double)MFMA_ROWS * (TILE_SEG_ALIGN - 1);
+    return std::max(std::ceil(nu / MFMA_UC), std::ceil(nnz / room));
+}
+
+MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, double min_reuse,
+                     double min_npc) {
     MfmaGate g;
     if (m == 0) return g;
     std::vector<int32_t> stamp((size_t)ncols, -1);
     const int64_t ntiles = (m + MFMA_ROWS - 1) / MFMA_ROWS;
     const int64_t ns = std::min<int64_t>(MFMA_GATE_SAMPLE, ntiles);
-    const int64_t room = MFMA_CAPA - (int64_t)MFMA_ROWS * (TILE_SEG_ALIGN - 1);
     double sum_r = 0.0, nz_taken = 0.0, ch_taken = 0.0, n_taken = 0.0;
     for (int64_t i = 0; i < ns; ++i) {
         const int64_t t = i * ntiles / ns;
@@ -995,9 +1019,9 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
         const double reuse = tile_reuse(rp, col, r0, r1, stamp, (int32_t)i, 0.0, &nu);
         sum_r += reuse;
         ++g.sampled;
-        if (reuse >= MFMA_TILE_REUSE) {
-            const double nnz = (double)(rp[r1] - rp[r0]);
-            const double ch = std::max(std::ceil((double)nu / MFMA_UC), std::ceil(nnz / (double)room));
+        const double nnz = (double)(rp[r1] - rp[r0]);
+        const double ch = mfma_chunks_est(nnz, (double)nu);
+        if (reuse >= min_reuse && nnz >= min_npc * ch) {
             nz_taken += nnz, ch_taken += ch, n_taken += 1.0;
             g.max_chunks = std::max(g.max_chunks, ch);
         }
@@ -1006,23 +1030,21 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
     g.r16 = sum_r / g.sampled;
     g.take = n_taken / g.sampled;
     const double scale = (double)ntiles / (double)ns;   // sampled slots -> all candidate slots
+    g.tiles = n_taken * scale;
     g.tile_nnz = nz_taken * scale;
     g.chunks = ch_taken * scale;
     return g;
 }
 
-// The gate.  Cost model (us per K panel of 32 columns), fitted on same-process A/B data (tools/mfma_ab.py,
-// profiles/r04/ab/):
-//   row kernel:   t_row(nnz, rows) = launch + nnz / R_ROW(reuse)     (a 256-B B row gathered per nonzero; dense
-//                 rows hit L2, so the rate grows with the tile reuse)
-//   tile kernel:  t_mfma = launch + max(chunks / (CHUNK_RATE * waves_in_flight), max_chunks * CHUNK_LAT)
-// Matrix-core tiles are taken when t_on = max(t_mfma, t_row(leftover)) beats t_off = t_row(all) by MFMA_MIN_GAIN.
-constexpr double MFMA_MIN_REUSE = 3.0;      // sampled 16-row reuse of the matrix (policy)
-constexpr int64_t MFMA_MIN_NNZ = 4000000;   // smaller launches lost 0.64-0.92x (too few waves, §6.17)
-void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k) {
-    (void)k;
-    g.verdict = ((m + MFMA_ROWS - 1) / MFMA_ROWS >= MFMA_MIN_TILES && nnz >= MFMA_MIN_NNZ && g.r16 >= MFMA_MIN_REUSE)
-                    ? 1 : 0;
+// The gate: the cost model above for the K columns in 32-column sub-panels.
+void mfma_cost(MfmaGate &g, int64_t nnz, int k) {
+    const double P = (double)k / 32.0;
+    g.t_off = MFMA_US_LAUNCH + (double)nnz * P * ROW_US_NNZ;
+    const double t_tiles = MFMA_US_LAUNCH + P * std::max(g.chunks * MFMA_US_CHUNK + g.tiles * MFMA_US_TILE,
+                                                         g.max_chunks * MFMA_US_CHAIN);
+    const double t_left = MFMA_US_LAUNCH + ((double)nnz - g.tile_nnz) * P * ROW_US_NNZ;
+    g.t_on = std::max(t_tiles, t_left);
+    g.verdict = (g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.t_off >= MFMA_MIN_GAIN * g.t_on) ? 1 : 0;
 }
 
 // Everything the inspector decides for (matrix, K), on the host: the plan, the tile plan, the block decomposition,
@@ -1147,9 +1169,10 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
                 const char *mthr = getenv("SPMM_HIP_MFMA_REUSE");
                 const bool force_all = forced > 0 || fm == 1;
                 const double treuse = (mthr && *mthr) ? atof(mthr) : force_all ? 1.0 : MFMA_TILE_REUSE;
-                d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max);
-                mfma_cost(d.gate, h->m, h->nnz, k);
-                if (mthr && *mthr && fm <= 0) d.gate.verdict = d.gate.r16 >= atof(mthr) ? 1 : 0;
+                const char *npc_env = getenv("SPMM_HIP_MFMA_NPC");   // measurement override of MFMA_TILE_NPC
+                const double npc = force_all ? 0.0 : (npc_env && *npc_env) ? atof(npc_env) : MFMA_TILE_NPC;
+                d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, treuse, npc);
+                mfma_cost(d.gate, h->nnz, k);
                 pl.tile_reuse = d.gate.r16;
                 if (gate_only) {
                     d.gate_only = true;
@@ -1158,8 +1181,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
                 }
                 if (force_all || fm == 2 || d.gate.verdict) {
                     tiles = build_tiles(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, MFMA_ROWS,
-                                        MFMA_UC, MFMA_CAPA, treuse, tp);
-                    if (tiles && !force_all && fm != 2 && (int64_t)tp.tiles.size() < MFMA_MIN_TILES / 2) tiles = false;
+                                        MFMA_UC, MFMA_CAPA, treuse, tp, INT32_MAX, INT32_MAX, npc);
                     if (tiles && !tile_tables_fit(tp)) tiles = false;
                     if (tiles) pl.tile_mfma = 1;
                 }
@@ -2131,6 +2153,24 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
         out[25] = (double)(fp >> 32);
     }
     out[23] = d.gate_only ? 1 : 0;
+    out[26] = d.gate.tiles;
+    return SPMM_HIP_OK;
+}
+
+int spmm_hip_debug_gate(int64_t nnz, int32_t k, const double *sample, double *out) {
+    if (!sample || !out || nnz < 0 || k < 1) return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
+    MfmaGate g;
+    g.sampled = (int)sample[0];
+    g.r16 = sample[1];
+    g.take = sample[2];
+    g.tiles = sample[3];
+    g.tile_nnz = sample[4];
+    g.chunks = sample[5];
+    g.max_chunks = sample[6];
+    mfma_cost(g, nnz, k);
+    out[0] = g.verdict;
+    out[1] = g.t_on;
+    out[2] = g.t_off;
     return SPMM_HIP_OK;
 }
 

@@ -55,7 +55,7 @@ def test_gate_from_sample_equals_full(S, line, k):
 def test_debug_plan_estimates(S):
     """The gate's sample estimates the built tiles: nonzeros in tiles within 5 %, chunks within 10 %."""
     A = S.generate(S.gen_params(LINES[0]))
-    d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32)
+    d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, 32, mfma=2)          # the gate forced open
     assert d["mode"] == "mfma"
     assert abs(d["est_tile_nnz"] / d["tile_nnz"] - 1) < 0.05
     assert abs(d["est_chunks"] / d["tile_chunks"] - 1) < 0.10
@@ -76,3 +76,13 @@ def test_debug_plan_rejects_bad_input(S):
         S.debug_plan(rp, np.zeros(2, np.int32), 4, 32)
     with pytest.raises(S.SpmmHipError):
         S.debug_plan(np.array([0, 1], np.int32), np.array([7], np.int32), 4, 32)
+
+
+@pytest.mark.parametrize("line", LINES[:3])
+def test_debug_gate_reproduces_plan_verdict(S, line):
+    """spmm_hip_debug_gate on the sample debug_plan reports gives debug_plan's own verdict and model times."""
+    A = S.generate(S.gen_params(line))
+    for k in (32, 64, 128):
+        d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, gate_only=True)
+        g = S.debug_gate(A.nnz, k, d)
+        assert g["gate"] == d["gate"] and g["t_on_us"] == d["t_on_us"] and g["t_off_us"] == d["t_off_us"]

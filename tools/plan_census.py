@@ -27,8 +27,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 sys.path.insert(0, str(ROOT))
 
-KEEP = ("mode", "gate", "r16", "take", "est_tile_nnz", "est_chunks", "max_chunks", "t_on_us", "t_off_us", "sampled",
-        "seq_max", "kw", "npanels")
+KEEP = ("mode", "gate", "r16", "take", "est_tiles", "est_tile_nnz", "est_chunks", "max_chunks", "t_on_us", "t_off_us",
+        "sampled", "seq_max", "kw", "npanels")
 
 
 def census_line(job):
