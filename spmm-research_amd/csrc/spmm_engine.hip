@@ -165,7 +165,7 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     const uint32_t pb = (uint32_t)std::min<uint64_t>((uint64_t)h->nslots * ld * sizeof(T), 0xFFFFFFFFull);
     auto go = [&](auto mode_c, auto xcd_c, auto vl_c) {
         spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
-                         decltype(vl_c)::value><<<h->nblk, WG, 0, s>>>(
+                         decltype(vl_c)::value><<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
             h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
             h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
     };
@@ -318,7 +318,8 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStr
     for (int p = 0; p < h->plan.npanels; ++p) {
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
-        if (h->nblk > 0) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
+        // ygrid: every panel of the row kernel in one launch (blockIdx.y = panel; equal panel widths, checked at plan)
+        if (h->nblk > 0 && (!h->plan.ygrid || p == 0)) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
         if (h->plan.ntile > 0 && !h->plan.tile_mfma) launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
     }
     if (h->nlong > 0 && !h->fuse) {
@@ -397,6 +398,10 @@ int split_length(const spmm_hip_t *h, int kw) {
 }
 
 constexpr int64_t PANEL_ROW_BYTES = 256;          // B bytes per row of one K panel
+constexpr int64_t SMALL_NNZ = 1000000;            // small-matrix panels (ygrid) below this many nonzeros
+#ifndef SMALL_KW_DEFAULT
+#define SMALL_KW_DEFAULT 0
+#endif
 constexpr double PANEL_MIN_B_BYTES = 128.0 * (1 << 20);  // B below half the Infinity Cache: no panels
 constexpr double PANEL_MIN_ROW_NNZ = 16.0;
 
@@ -1108,6 +1113,15 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         const double x = span * 2.0 * WIN_LINE / WIN_L2_BYTES;
         if (crs < NARROW_MAX_CRS && x >= NARROW_MIN_SPAN_L2 && x <= NARROW_MAX_SPAN_L2) pl.kw /= 2;
     }
+    // small matrices: a launch of a few hundred blocks leaves most of the 256 CUs idle and its rows'
+    // gather chains exposed; narrower K panels, all in ONE launch (blockIdx.y = panel), give more blocks and more
+    // vector-lane groups per row.  SPMM_HIP_SMALL_KW=<cols> sets the panel width (0: off).
+    {
+        const int small_kw = env_int("SPMM_HIP_SMALL_KW", SMALL_KW_DEFAULT);
+        if (h->var.panel_k <= 0 && panel_env <= 0 && small_kw > 0 && h->nnz > 0 && h->nnz < SMALL_NNZ &&
+            pl.kw == k && k > small_kw && k % small_kw == 0)
+            pl.kw = small_kw, pl.ygrid = 1;
+    }
     pl.npanels = (k + pl.kw - 1) / pl.kw;
     // block capacity and split length
     int vec, g;
@@ -1270,6 +1284,9 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         pl.nseg = (int64_t)in.vrow_ptr.size() - 1;
     }
     const int nblk = (int)in.blk.size();
+    // one-launch panels: not with column windows (separate launches then); split rows are combined by the separate
+    // combine kernel afterwards (the fused combine counts one row's pieces within one panel)
+    if (pl.ygrid && (W > 0 || k % pl.kw != 0)) pl.ygrid = 0;
     // vector lanes when the staged blocks hold fewer rows than row groups (long rows at small K), and
     // the exact-row mask: rows <= T whose every virtual row sits in a block with L = 1
     {
@@ -1332,7 +1349,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
     {
         std::vector<int32_t> &slot_lr = d.slot_lr;
         const int nslots = in.nslots;
-        bool fuse = nslots > 0 && W == 0 && env_int("SPMM_HIP_FUSE", 1) != 0 &&
+        bool fuse = nslots > 0 && W == 0 && !pl.ygrid && env_int("SPMM_HIP_FUSE", 1) != 0 &&
                     (uint64_t)nslots * (uint64_t)k * h->vsize < (1ULL << 32);
         if (fuse) {
             slot_lr.assign((size_t)nslots, -1);
@@ -1375,7 +1392,7 @@ uint64_t plan_fingerprint(const Draft &d) {
         for (size_t i = 0; i < n; ++i) x = (x ^ c[i]) * 1099511628211ULL;
     };
     const Plan &p = d.pl;
-    const int64_t f[] = {p.k, p.kw, p.npanels, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
+    const int64_t f[] = {p.k, p.kw, p.npanels, p.ygrid, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
                          p.xcd, p.lmax, p.exact_rows, p.ntile, p.tile_xcd, p.tile_wide, p.tile_mfma, p.tile_rows,
                          p.tile_nnz, p.tile_chunks, (int64_t)d.fuse};
     mix(f, sizeof(f));

@@ -33,6 +33,7 @@ int fail(int status, const std::string &what);  // records the detail, returns s
 struct Plan {
     int k = -1;
     int kw = 0, npanels = 0;   // panel width (columns) and count
+    int ygrid = 0;             // 1 = the row kernel runs all panels in one launch (blockIdx.y = panel)
     int seq_max = 0;           // T: rows of <= T nonzeros are one chain (exact)
     int piece = 0;             // rows longer than T are cut into pieces of this many nonzeros (T, or GAP_SEQ_MAX)
     int cap = 0;               // block capacity (nonzeros)

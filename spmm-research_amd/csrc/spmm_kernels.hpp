@@ -261,6 +261,12 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
 
     const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int tid = threadIdx.x;
+    if (blockIdx.y > 0) {       // K panels of one launch (small matrices, plan.ygrid): panel blockIdx.y of width kw
+        const uint32_t off = blockIdx.y * (uint32_t)kw;
+        B += off, C += off;
+        b_bytes -= off * (uint32_t)sizeof(T);
+        if (P) P += off, p_bytes -= off * (uint32_t)sizeof(T);   // partial slots [nslots][ld]; combined afterwards
+    }
     __shared__ int s_ndone;
     if (tid == 0) s_ndone = 0;
     const int4 rr = blk[b];                                 // {first, end | flags, vrow_ptr[first], vrow_ptr[end]}

@@ -77,3 +77,32 @@ def test_tiny_row_windows_bitwise(env, monkeypatch):
     assert inf0[12] == 1
     assert np.array_equal(Cw.view(np.int64), C0.view(np.int64))
     assert sample_rows_exact(O, A, B, Cw, ex) > 1000
+
+
+# Small matrices: narrower K panels of the row kernel, all in ONE launch (blockIdx.y = panel).  Every
+# C entry is still the same chain for exact rows (panels only choose which columns a block computes), so the output
+# must equal the one-panel plan on every row both plans compute exactly, and be within 1e-10 normwise elsewhere
+# (vector lanes / split rows; the separate combine kernel sums the split rows of every panel).
+SMALL = ["698 698 500 166.6667 normal random 0.05 0 0.05 0.5 14",          # 4-row blocks, vector lanes
+         "65535 65535 5 1.6667 normal random 0.3 0 0.5 0.05 14",           # many short rows
+         "3483 3483 100 33.3333 normal random 0.6 1000 0.95 0.95 14"]      # a skewed row: split, combined
+
+
+@pytest.mark.parametrize("line", SMALL)
+@pytest.mark.parametrize("kw", [8, 16])
+@pytest.mark.parametrize("k", [32, 128])
+def test_small_matrix_one_launch_panels(env, monkeypatch, line, kw, k):
+    torch, S, O = env
+    A = S.generate(S.gen_params(line))
+    B0, C0, inf0, ex0 = run_device(torch, S, A, k, monkeypatch, SPMM_HIP_SMALL_KW=0)
+    B1, C1, inf1, ex1 = run_device(torch, S, A, k, monkeypatch, SPMM_HIP_SMALL_KW=kw)
+    assert np.array_equal(B0, B1)
+    assert inf1[10] == kw and inf1[11] == k // kw
+    assert np.isfinite(C1).all()
+    both = ex0 & ex1
+    assert np.array_equal(C1[both].view(np.int64), C0[both].view(np.int64))
+    x = np.ascontiguousarray(B0.T).ravel()
+    g, absdot = O.gold(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+    assert O.normwise_ok(C1, g, absdot, 1e-10).all()
+    seq = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+    assert np.array_equal(C1[ex1].view(np.int64), seq[ex1].view(np.int64))

@@ -81,7 +81,10 @@ def main():
                     torch.cuda.synchronize()
                     ts[n].append(e0.elapsed_time(e1) / args.iters)
             n0, n1 = modes[0][0], modes[-1][0]
-            ex = torch.from_numpy(hs[n0].exact_rows() & hs[n1].exact_rows()).to(dev)
+            exm = hs[n0].exact_rows()
+            for h_ in hs.values():
+                exm = exm & h_.exact_rows()
+            ex = torch.from_numpy(exm).to(dev)
             same = all(bool(torch.equal(Cs[n][ex].view(torch.int64), Cs[n0][ex].view(torch.int64))) for n in hs)
             ti = hs[n1].tile_info()
             ba = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64)
