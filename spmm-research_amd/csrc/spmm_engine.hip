@@ -302,7 +302,10 @@ void launch_mfma(spmm_hip_t *h, const T *B, T *C, int ld, int k0, int kw, hipStr
         };
         using N1 = std::integral_constant<int, 1>;
         using N2 = std::integral_constant<int, 2>;
-        if (h->plan.tile_xcd) np == 2 ? go(std::true_type(), N2()) : go(std::true_type(), N1());
+        if (std::is_same_v<T, double> && np == 1 && h->plan.tile_xcd && env_int("SPMM_HIP_MFMA_CHECK", 1) == 0)
+            spmm_mfma_tile_kernel<T, true, 1, false><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk,
+                h->d_tcol, (const T *)h->d_tval, h->d_tlidx, B + k1, bb, C + k1, ld);   // measurement only
+        else if (h->plan.tile_xcd) np == 2 ? go(std::true_type(), N2()) : go(std::true_type(), N1());
         else np == 2 ? go(std::false_type(), N2()) : go(std::false_type(), N1());
         k1 += 32 * np;
     }

@@ -95,7 +95,8 @@ template <> struct MfmaT<float> {
     __device__ static float fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 };
 
-template <typename T, bool XCD, int NP>
+// CHECK = false: no exact-range check (measurement only: SPMM_HIP_MFMA_CHECK=0 prices the check; never a product path)
+template <typename T, bool XCD, int NP, bool CHECK = true>
 __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm_mfma_tile_kernel(
     const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
     const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, uint32_t b_bytes,
@@ -214,12 +215,12 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) {
             if (st < ns) {
-                emin = min(emin, M::fexp(a[st]));
+                if constexpr (CHECK) emin = min(emin, M::fexp(a[st]));
 #pragma unroll
                 for (int p = 0; p < NP; ++p) {
                     T bb[2];
                     __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
-                    emin = min(emin, min(M::fexp(bb[0]), M::fexp(bb[1])));
+                    if constexpr (CHECK) emin = min(emin, min(M::fexp(bb[0]), M::fexp(bb[1])));
                     acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
                     acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
                 }
@@ -228,12 +229,14 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
         }
         // an operand below the range, or a non-finite accumulator (Inf/NaN in B -- a panel zero times it is NaN --,
         // or an overflow): the tile goes to the sparse chain
-        bad = emin < M::MIN_EXP;
+        if constexpr (CHECK) {
+            bad = emin < M::MIN_EXP;
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
+            for (int p = 0; p < NP; ++p)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) bad |= !__builtin_isfinite(acc[p][0][i]) || !__builtin_isfinite(acc[p][1][i]);
-        if (__builtin_amdgcn_ballot_w64(bad)) break;
+                for (int i = 0; i < 4; ++i) bad |= !__builtin_isfinite(acc[p][0][i]) || !__builtin_isfinite(acc[p][1][i]);
+            if (__builtin_amdgcn_ballot_w64(bad)) break;
+        }
         load_tcol(min(c + 2, tl.w - 1));
     }
     if (__builtin_amdgcn_ballot_w64(bad)) {      // outside the exact range: the whole tile by the sparse chain
