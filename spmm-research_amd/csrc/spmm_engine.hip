@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -987,7 +988,9 @@ constexpr double MFMA_US_CHUNK = 1.55e-3;
 constexpr double MFMA_US_TILE = 2.0e-3;
 constexpr double MFMA_US_CHAIN = 4.5;
 constexpr double MFMA_US_LAUNCH = 6.0;
-constexpr double ROW_US_NNZ = 12.0e-6;
+constexpr double ROW_US_NNZ = 30.0e-6;       // x reuse^-ROW_REUSE_EXP x (kw / 32)^-ROW_KW_EXP
+constexpr double ROW_REUSE_EXP = 0.5;       // similar rows hit L2: the gather gets cheaper with the sampled reuse
+constexpr double ROW_KW_EXP = 0.15;         // an unpanelled launch reads A once for all its columns
 constexpr double MFMA_TILE_NPC = 150.0;     // nonzeros per chunk for a tile to be taken
 constexpr double MFMA_MIN_GAIN = 1.10;      // predicted t_off / t_on
 constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
@@ -1045,12 +1048,14 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
 }
 
 // The gate: the cost model above for the K columns in 32-column sub-panels.
-void mfma_cost(MfmaGate &g, int64_t nnz, int k) {
+void mfma_cost(MfmaGate &g, int64_t nnz, int k, int kw) {
     const double P = (double)k / 32.0;
-    g.t_off = MFMA_US_LAUNCH + (double)nnz * P * ROW_US_NNZ;
+    const double r_row = ROW_US_NNZ * std::pow(std::max(g.r16, 1.0), -ROW_REUSE_EXP) *
+                         std::pow((double)std::max(kw, 1) / 32.0, -ROW_KW_EXP);
+    g.t_off = MFMA_US_LAUNCH + (double)nnz * P * r_row;
     const double t_tiles = MFMA_US_LAUNCH + P * std::max(g.chunks * MFMA_US_CHUNK + g.tiles * MFMA_US_TILE,
                                                          g.max_chunks * MFMA_US_CHAIN);
-    const double t_left = MFMA_US_LAUNCH + ((double)nnz - g.tile_nnz) * P * ROW_US_NNZ;
+    const double t_left = MFMA_US_LAUNCH + ((double)nnz - g.tile_nnz) * P * r_row;
     g.t_on = std::max(t_tiles, t_left);
     g.verdict = (g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.t_off >= MFMA_MIN_GAIN * g.t_on) ? 1 : 0;
 }
@@ -1189,7 +1194,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
                 const char *npc_env = getenv("SPMM_HIP_MFMA_NPC");   // measurement override of MFMA_TILE_NPC
                 const double npc = force_all ? 0.0 : (npc_env && *npc_env) ? atof(npc_env) : MFMA_TILE_NPC;
                 d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, treuse, npc);
-                mfma_cost(d.gate, h->nnz, k);
+                mfma_cost(d.gate, h->nnz, k, pl.kw);
                 pl.tile_reuse = d.gate.r16;
                 if (gate_only) {
                     d.gate_only = true;
@@ -2177,8 +2182,8 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     return SPMM_HIP_OK;
 }
 
-int spmm_hip_debug_gate(int64_t nnz, int32_t k, const double *sample, double *out) {
-    if (!sample || !out || nnz < 0 || k < 1) return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
+int spmm_hip_debug_gate(int64_t nnz, int32_t k, int32_t kw, const double *sample, double *out) {
+    if (!sample || !out || nnz < 0 || k < 1 || kw < 1) return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
     MfmaGate g;
     g.sampled = (int)sample[0];
     g.r16 = sample[1];
@@ -2187,7 +2192,7 @@ int spmm_hip_debug_gate(int64_t nnz, int32_t k, const double *sample, double *ou
     g.tile_nnz = sample[4];
     g.chunks = sample[5];
     g.max_chunks = sample[6];
-    mfma_cost(g, nnz, k);
+    mfma_cost(g, nnz, k, kw);
     out[0] = g.verdict;
     out[1] = g.t_on;
     out[2] = g.t_off;

@@ -74,7 +74,7 @@ def features(args):
 def model(F, c):
     """t_on, t_off (us) for feature rows F with constants c (mirrors mfma_cost)."""
     P = F["k"] / 32.0
-    r_row = c["row_us_nnz"]
+    r_row = c["row_us_nnz"] * np.maximum(F["r16"], 1.0) ** -c["row_reuse_exp"] * (F["kw"] / 32.0) ** -c["row_kw_exp"]
     t_off = c["launch"] + F["nnz"] * P * r_row
     t_tiles = c["launch"] + P * np.maximum(F["est_chunks"] * c["us_chunk"] + F["est_tiles"] * c["us_tile"],
                                            F["max_chunks"] * c["us_chain"])
@@ -90,21 +90,30 @@ def fit(args):
         feats[(d["gen"], d["k"])] = d
     keys = [k for k in ab if k in feats and ab[k]["tile_mode"] == "mfma"]
     F = {f: np.array([feats[k][f] if f in feats[k] else ab[k][f] for k in keys], float)
-         for f in ("k", "nnz", "est_chunks", "est_tiles", "est_tile_nnz", "max_chunks", "r16")}
+         for f in ("k", "nnz", "est_chunks", "est_tiles", "est_tile_nnz", "max_chunks", "r16", "kw")}
     t_on = np.array([ab[k]["ms"] * 1e3 for k in keys])
     t_off = np.array([ab[k]["ms_base"] * 1e3 for k in keys])
     P = F["k"] / 32.0
-    # row kernel: t_off = launch + r * nnz * P   (least squares in relative error)
-    X = np.stack([np.ones_like(t_off), F["nnz"] * P], 1) / t_off[:, None]
-    launch, r_row = np.linalg.lstsq(X, np.ones_like(t_off), rcond=None)[0]
-    # tile kernel, on lines whose tiles hold >= 90 % of the nonzeros (t_on ~ the tile kernel)
-    sel = F["est_tile_nnz"] >= 0.9 * F["nnz"]
-    Xt = np.stack([np.ones(sel.sum()), P[sel] * F["est_chunks"][sel], P[sel] * F["est_tiles"][sel]], 1) / t_on[sel, None]
-    l2, a, b = np.linalg.lstsq(Xt, np.ones(sel.sum()), rcond=None)[0]
-    chain = np.median((t_on[sel] - l2) / (P[sel] * F["max_chunks"][sel]))
-    c = {"launch": float(launch), "row_us_nnz": float(r_row), "us_chunk": float(a), "us_tile": float(b),
-         "us_chain": float(chain)}
-    print(json.dumps({"fit": c, "lines": len(keys), "tile_lines": int(sel.sum())}))
+    from scipy.optimize import least_squares
+    # row kernel: t_off = launch + r * nnz * P (relative error)
+    def res_off(x):
+        c = {"launch": x[0], "row_us_nnz": x[1], "row_reuse_exp": x[2], "row_kw_exp": x[3], "us_chunk": 1.0,
+             "us_tile": 0.0, "us_chain": 0.0}
+        return np.log(model(F, c)[1] / t_off)
+    r0 = least_squares(res_off, [10.0, 12e-6, 0.1, 0.1], bounds=([0, 0, -1, -1], [100, 1e-3, 2, 2])).x
+    # the shipped time: max(tile kernel, leftover rows) with the tile kernel's launch + max(throughput, chain)
+    def res_on(x):
+        c = {"launch": r0[0], "row_us_nnz": r0[1], "row_reuse_exp": r0[2], "row_kw_exp": r0[3], "us_chunk": x[0],
+             "us_tile": x[1], "us_chain": x[2]}
+        m_on, _ = model(F, c)
+        return np.log(m_on / t_on)
+    x = least_squares(res_on, [1.6e-3, 1e-3, 4.5], bounds=([0, 0, 0], [1e-2, 1e-2, 50]), loss="soft_l1").x
+    c = {"launch": float(r0[0]), "row_us_nnz": float(r0[1]), "row_reuse_exp": float(r0[2]),
+         "row_kw_exp": float(r0[3]), "us_chunk": float(x[0]), "us_tile": float(x[1]), "us_chain": float(x[2])}
+    m_on, m_off = model(F, c)
+    print(json.dumps({"fit": c, "lines": len(keys),
+                      "rms_log_err_on": float(np.sqrt(np.mean(np.log(m_on / t_on) ** 2))),
+                      "rms_log_err_off": float(np.sqrt(np.mean(np.log(m_off / t_off) ** 2)))}))
     m_on, m_off = model(F, c)
     sp = t_off / t_on
     pred = m_off / m_on

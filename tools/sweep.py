@@ -151,6 +151,16 @@ def cpu_baseline(O, A, vals, x_col, k, budget_s, cores):
             "cpu_cores": cores}
 
 
+def read_pairs(f):
+    """'K<TAB>generator line' text file -> {(line, K)}."""
+    out = set()
+    for l in Path(f).read_text().splitlines():
+        if "\t" in l:
+            k_, g_ = l.split("\t", 1)
+            out.add((g_.strip(), int(k_)))
+    return out
+
+
 class env_set:
     """Set ENV=V,ENV=V for the duration of a with-block (the engine reads its policy overrides at plan time)."""
     def __init__(self, spec):
@@ -225,6 +235,10 @@ def main():
     ap.add_argument("--census", default=None,
                     help="keep only the (line, K) pairs whose census record (tools/plan_census.py) has mode == --census-mode")
     ap.add_argument("--census-mode", default="mfma")
+    ap.add_argument("--pairs", default=None,
+                    help="text file of 'K<TAB>generator line' pairs: keep only these (e.g. the census's changed set)")
+    ap.add_argument("--skip-pairs", default=None,
+                    help="text file of 'K<TAB>generator line' pairs already swept (resume across calls)")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "sweep.jsonl"))
     args = ap.parse_args()
     if args.workers > 1 and args.worker is None:
@@ -255,6 +269,10 @@ def main():
                 done.add((d["gen"], d["k"], d["dtype"]))
             except Exception:
                 pass
+    if args.skip_pairs and Path(args.skip_pairs).exists():
+        for g_, k_ in read_pairs(args.skip_pairs):
+            for dt_ in dtypes:
+                done.add((g_, k_, dt_))
     done_idx = set()
     if args.done and Path(args.done).exists():
         done_idx = {int(x) for x in Path(args.done).read_text().split()}
@@ -270,6 +288,8 @@ def main():
             d = json.loads(l)
             if d.get("mode") == args.census_mode:
                 census.add((d["gen"], int(d["k"])))
+    if args.pairs:
+        census = read_pairs(args.pairs) if census is None else census & read_pairs(args.pairs)
     work = []
     for idx, line in idx_lines:
         if idx in done_idx:
