@@ -991,7 +991,7 @@ constexpr double MFMA_US_LAUNCH = 6.0;
 constexpr double ROW_US_NNZ = 30.0e-6;       // x reuse^-ROW_REUSE_EXP x (kw / 32)^-ROW_KW_EXP
 constexpr double ROW_REUSE_EXP = 0.5;       // similar rows hit L2: the gather gets cheaper with the sampled reuse
 constexpr double ROW_KW_EXP = 0.15;         // an unpanelled launch reads A once for all its columns
-constexpr double MFMA_TILE_NPC = 150.0;     // nonzeros per chunk for a tile to be taken
+constexpr double MFMA_TILE_NPC = 96.0;      // nonzeros per chunk for a tile to be taken
 constexpr double MFMA_MIN_GAIN = 1.10;      // predicted t_off / t_on
 constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
 struct MfmaGate {
