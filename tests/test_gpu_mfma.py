@@ -131,14 +131,22 @@ def test_mfma_update_values(env, monkeypatch):
 
 
 def test_mfma_policy_dense_band(env, monkeypatch):
-    """Default policy: the 22354 x 500 dense band (16-row reuse ~ 5) takes matrix-core tiles at K = 32 and 128; a
+    """Default policy: the plan takes matrix-core tiles exactly when the gate (spmm_hip_debug_plan, host only) says
+    so -- on dense bands at K = 32 and 128 -- and the gate forced open (SPMM_HIP_MFMA=2) always takes them there; a
     low-reuse matrix does not."""
     torch, S, O = env
-    A = S.generate(S.gen_params("22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14"))
-    for k in (32, 128):
-        mf = handle(S, A, A.values, k, monkeypatch, {})
-        assert mf.tile_info()["mode"] == "mfma", k
-        mf.close()
+    for line in ("22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14",
+                 "111476 111476 100 33.3333 normal random 0.3 0 0.05 0.95 14"):
+        A = S.generate(S.gen_params(line))
+        for k in (32, 128):
+            d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, gate_only=True)
+            mf = handle(S, A, A.values, k, monkeypatch, {})
+            assert mf.tile_info()["mode"] == ("mfma" if d["gate"] else mf.tile_info()["mode"]), (line, k)
+            assert (mf.tile_info()["mode"] == "mfma") == bool(d["gate"]), (line, k)
+            mf.close()
+            mf = handle(S, A, A.values, k, monkeypatch, {"SPMM_HIP_MFMA": "2"})
+            assert mf.tile_info()["mode"] == "mfma", (line, k)
+            mf.close()
     L = S.generate(S.gen_params("200000 200000 10 3.3333 normal random 0.6 0 0.05 0.05 14"))
     mf = handle(S, L, L.values, 32, monkeypatch, {})
     assert mf.tile_info()["mode"] != "mfma"
