@@ -272,7 +272,7 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
  * ([12]); out[3] = {verdict, model
  * time with matrix-core tiles (us), without (us)}.  Lets a census re-decide with this library's constants without
  * regenerating the matrices (tools/plan_census.py --regate). */
-int spmm_hip_debug_gate(int64_t nnz, int32_t k, int32_t kw, const double *sample, double *out);
+int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, const double *sample, double *out);
 
 const char *spmm_hip_strerror(int status);
 const char *spmm_hip_last_error_detail(void);

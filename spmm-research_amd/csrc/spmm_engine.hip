@@ -117,7 +117,7 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 void free_plan(spmm_hip_t *h) {
     void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
                   h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr, h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg,
-                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm};
+                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm, h->d_mflag};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
@@ -130,6 +130,7 @@ void free_plan(spmm_hip_t *h) {
     h->d_tval = nullptr;
     h->d_tstamps = nullptr;
     h->d_wperm = h->d_tperm = nullptr;
+    h->d_mflag = nullptr;
     h->nwperm = h->ntperm = 0;
     h->fuse = false;
     h->win_blk.clear();
@@ -293,20 +294,25 @@ template <typename T>
 void launch_mfma(spmm_hip_t *h, const T *B, T *C, int ld, int k0, int kw, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
     const int np_max = env_int("SPMM_HIP_MFMA_NP", 2) >= 2 ? 2 : 1;
+    // B's exact-range check (spmm_mfma.hpp) into mflag[1], on the tiles' stream before their launch
+    {
+        const int64_t n = (int64_t)h->ncols * ld - k0;
+        const int64_t nv = (n + 16 / (int64_t)sizeof(T) - 1) / (16 / (int64_t)sizeof(T));
+        const unsigned rg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, (nv + WG - 1) / WG));
+        (void)hipMemsetAsync(h->d_mflag + 1, 0, sizeof(int), s);
+        mfma_range_kernel<T><<<rg, WG, 0, s>>>(B, n, h->d_mflag + 1);
+    }
     for (int k1 = 0; k1 + 32 <= kw;) {
         const int np = (np_max >= 2 && k1 + 64 <= kw) ? 2 : 1;
         const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)(k0 + k1)) * sizeof(T));
         auto go = [&](auto xcd_c, auto np_c) {
             spmm_mfma_tile_kernel<T, decltype(xcd_c)::value, decltype(np_c)::value><<<grid, WG, 0, s>>>(
                 h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const T *)h->d_tval, h->d_tlidx, B + k1, bb,
-                C + k1, ld);
+                C + k1, ld, h->d_mflag);
         };
         using N1 = std::integral_constant<int, 1>;
         using N2 = std::integral_constant<int, 2>;
-        if (std::is_same_v<T, double> && np == 1 && h->plan.tile_xcd && env_int("SPMM_HIP_MFMA_CHECK", 1) == 0)
-            spmm_mfma_tile_kernel<T, true, 1, false><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk,
-                h->d_tcol, (const T *)h->d_tval, h->d_tlidx, B + k1, bb, C + k1, ld);   // measurement only
-        else if (h->plan.tile_xcd) np == 2 ? go(std::true_type(), N2()) : go(std::true_type(), N1());
+        if (h->plan.tile_xcd) np == 2 ? go(std::true_type(), N2()) : go(std::true_type(), N1());
         else np == 2 ? go(std::false_type(), N2()) : go(std::false_type(), N1());
         k1 += 32 * np;
     }
@@ -977,22 +983,28 @@ double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64
 // (reuse >= MFMA_TILE_REUSE) scaled to the matrix give the work of the tile kernel and of the row kernel on the same
 // rows, priced by mfma_cost (measured constants).
 constexpr int MFMA_GATE_SAMPLE = 256;
-// The tile kernel's cost model (us; fitted on same-process A/B data, tools/fit_mfma_gate.py).  Per
-// 32-column sub-panel the tile kernel streams each chunk's B rows and MFMAs at a chip-wide rate (MFMA_US_CHUNK per
-// chunk, MFMA_US_TILE per tile for its prologue / epilogue) unless it has too few tiles to fill the chip, when the
-// longest tiles' chunk chains bound it (MFMA_US_CHAIN per chunk); the row kernel gathers one B row per nonzero per
-// sub-panel (ROW_US_NNZ).  A tile is worth a dense panel product when its nonzeros per chunk reach
-// MFMA_TILE_NPC; a matrix takes matrix-core tiles when the model's time with them (tiles beside the leftover rows)
-// beats the row kernel's by MFMA_MIN_GAIN.
-constexpr double MFMA_US_CHUNK = 1.55e-3;
-constexpr double MFMA_US_TILE = 2.0e-3;
-constexpr double MFMA_US_CHAIN = 4.5;
-constexpr double MFMA_US_LAUNCH = 6.0;
-constexpr double ROW_US_NNZ = 30.0e-6;       // x reuse^-ROW_REUSE_EXP x (kw / 32)^-ROW_KW_EXP
-constexpr double ROW_REUSE_EXP = 0.5;       // similar rows hit L2: the gather gets cheaper with the sampled reuse
-constexpr double ROW_KW_EXP = 0.15;         // an unpanelled launch reads A once for all its columns
+// The tile kernel's cost model (us; fitted on same-process A/B data: tools/fit_mfma_gate.py on 598 medium-dataset
+// (line, K) pairs with the gate forced open, profiles/r04/s_c/).  Per 32-column sub-panel the tile
+// kernel streams each chunk's B rows and MFMAs at a chip-wide rate (MFMA_US_CHUNK per chunk, MFMA_US_TILE per tile for
+// its prologue / epilogue) unless it has too few tiles to fill the chip, when the longest tile's chunk chain bounds it
+// (MFMA_US_CHAIN per chunk).  The row kernel gathers one B row per nonzero per sub-panel (ROW_US_NNZ, cheaper for
+// similar rows -- L2 hits -- and for unpanelled launches that read A once for all columns) plus a per-row cost (C
+// store, row setup).  The tile-kernel constants are the fit's times 0.9: the exact-range check left the MFMA loop
+// afterwards (nochk / checked = 0.88-0.89, profiles/r04/s_b/kt.log).  A tile is taken when it brings at least
+// MFMA_TILE_NPC nonzeros per chunk; a matrix takes matrix-core tiles when they hold MFMA_MIN_TILE_FRAC of its
+// nonzeros and the model's time with them (tiles beside the leftover rows) beats the row kernel's by MFMA_MIN_GAIN.
+constexpr double MFMA_US_CHUNK = 1.385e-3;
+constexpr double MFMA_US_TILE = 1.36e-3;
+constexpr double MFMA_US_CHAIN = 1.01;
+constexpr double MFMA_US_LAUNCH = 22.0;
+constexpr double ROW_US_LAUNCH = 7.2;
+constexpr double ROW_US_NNZ = 1.877e-5;     // x reuse^-ROW_REUSE_EXP x (kw / 32)^-ROW_KW_EXP
+constexpr double ROW_REUSE_EXP = 0.148;
+constexpr double ROW_KW_EXP = 0.200;
+constexpr double ROW_US_ROW = 7.05e-5;
 constexpr double MFMA_TILE_NPC = 96.0;      // nonzeros per chunk for a tile to be taken
-constexpr double MFMA_MIN_GAIN = 1.10;      // predicted t_off / t_on
+constexpr double MFMA_MIN_TILE_FRAC = 0.9;  // partial coverage lost in the fit sample (tiles beside busy row blocks)
+constexpr double MFMA_MIN_GAIN = 1.30;      // in the fit sample: no taken line below 0.95x, every class >= 1.04x
 constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
 struct MfmaGate {
     int sampled = 0;          // candidate tiles sampled (all rows <= T, not empty)
@@ -1048,16 +1060,18 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
 }
 
 // The gate: the cost model above for the K columns in 32-column sub-panels.
-void mfma_cost(MfmaGate &g, int64_t nnz, int k, int kw) {
+void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k, int kw) {
     const double P = (double)k / 32.0;
     const double r_row = ROW_US_NNZ * std::pow(std::max(g.r16, 1.0), -ROW_REUSE_EXP) *
                          std::pow((double)std::max(kw, 1) / 32.0, -ROW_KW_EXP);
-    g.t_off = MFMA_US_LAUNCH + (double)nnz * P * r_row;
+    g.t_off = ROW_US_LAUNCH + P * ((double)nnz * r_row + (double)m * ROW_US_ROW);
     const double t_tiles = MFMA_US_LAUNCH + P * std::max(g.chunks * MFMA_US_CHUNK + g.tiles * MFMA_US_TILE,
                                                          g.max_chunks * MFMA_US_CHAIN);
-    const double t_left = MFMA_US_LAUNCH + ((double)nnz - g.tile_nnz) * P * r_row;
+    const double left_rows = std::max((double)m - (double)MFMA_ROWS * g.tiles, 0.0);
+    const double t_left = ROW_US_LAUNCH + P * (((double)nnz - g.tile_nnz) * r_row + left_rows * ROW_US_ROW);
     g.t_on = std::max(t_tiles, t_left);
-    g.verdict = (g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.t_off >= MFMA_MIN_GAIN * g.t_on) ? 1 : 0;
+    g.verdict = (g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.tile_nnz >= MFMA_MIN_TILE_FRAC * (double)nnz &&
+                 g.t_off >= MFMA_MIN_GAIN * g.t_on) ? 1 : 0;
 }
 
 // Everything the inspector decides for (matrix, K), on the host: the plan, the tile plan, the block decomposition,
@@ -1194,7 +1208,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
                 const char *npc_env = getenv("SPMM_HIP_MFMA_NPC");   // measurement override of MFMA_TILE_NPC
                 const double npc = force_all ? 0.0 : (npc_env && *npc_env) ? atof(npc_env) : MFMA_TILE_NPC;
                 d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, treuse, npc);
-                mfma_cost(d.gate, h->nnz, k, pl.kw);
+                mfma_cost(d.gate, h->m, h->nnz, k, pl.kw);
                 pl.tile_reuse = d.gate.r16;
                 if (gate_only) {
                     d.gate_only = true;
@@ -1648,6 +1662,20 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                     for (int u = 0; u < MFMA_UC; ++u)
                         tcolT[(size_t)ci * MFMA_UC + (u % 4) * MFMA_KS + u / 4] = tp.tcol[(size_t)ch.x + std::min(u, ch.y - 1)];
                 }
+            // A's exact range (spmm_mfma.hpp): mflag[0] = some tile value outside it; mflag[1] is B's, per launch
+            int mflag[2] = {0, 0};
+            for (size_t q = 0; q < nz && !mflag[0]; ++q) {
+                if (tp.perm[q] < 0) continue;
+                double v;
+                if (h->vsize == 8) std::memcpy(&v, &tval[q * 8], 8);
+                else { float f; std::memcpy(&f, &tval[q * 4], 4); v = f; }
+                int ex = 0;
+                (void)std::frexp(v, &ex);
+                const int lo = h->vsize == 8 ? MfmaT<double>::MIN_EXP : MfmaT<float>::MIN_EXP;
+                const int hi = h->vsize == 8 ? MfmaT<double>::MAX_EXP : MfmaT<float>::MAX_EXP;
+                mflag[0] = !std::isfinite(v) || (v != 0.0 && (ex < lo || ex > hi));
+            }
+            if (e == hipSuccess) e = alloc_copy((void **)&h->d_mflag, mflag, sizeof(mflag));
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tiles, tp.tiles.data(), tp.tiles.size() * sizeof(int4));
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tchunk, tp.chunks.data(), tp.chunks.size() * sizeof(int4));
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tcol, tcolT.data(), tcolT.size() * 4);
@@ -1829,31 +1857,41 @@ int spmm_hip_run_device_batch(int32_t count, spmm_hip_t *const *hs, const void *
 
 namespace {
 // dst[q] = perm[q] >= 0 ? src[perm[q]] : 0 (the window-major / tile chunk-major copies of A's values)
+// flag != nullptr (matrix-core tiles): also sets *flag when a gathered value lies outside the exact range
+// (spmm_mfma.hpp, mflag[0])
 template <typename T>
 __global__ __launch_bounds__(WG) void gather_values_kernel(const T *__restrict__ src, const int32_t *__restrict__ perm,
-                                                           T *__restrict__ dst, int64_t n) {
+                                                           T *__restrict__ dst, int64_t n, int *__restrict__ flag) {
     const int64_t q = (int64_t)blockIdx.x * WG + threadIdx.x;
+    bool bad = false;
     if (q < n) {
         const int32_t j = perm[q];
-        dst[q] = j >= 0 ? src[j] : T(-0.0);    // padding: -0 (LDS tiles: fma(-0, +0, acc) == acc, -0 kept)
+        const T v = j >= 0 ? src[j] : T(-0.0);    // padding: -0 (LDS tiles: fma(-0, +0, acc) == acc, -0 kept)
+        dst[q] = v;
+        if (flag) {
+            const int ex = MfmaT<T>::fexp(v);
+            bad = !__builtin_isfinite(v) || (v != T(0) && (ex < MfmaT<T>::MIN_EXP || ex > MfmaT<T>::MAX_EXP));
+        }
     }
+    if (flag && __builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 int update_values(spmm_hip_t *h, const void *vals, hipMemcpyKind kind, hipStream_t s) {
     if (h->nnz == 0) return SPMM_HIP_OK;
     HIPCHK(hipMemcpyAsync(h->d_val, vals, (size_t)h->nnz * h->vsize, kind, s));
-    auto gather = [&](const int32_t *perm, void *dst, int64_t n) -> int {
+    auto gather = [&](const int32_t *perm, void *dst, int64_t n, int *flag) -> int {
         if (!perm || n == 0) return SPMM_HIP_OK;
         const unsigned nb = (unsigned)((n + WG - 1) / WG);
+        if (flag) HIPCHK(hipMemsetAsync(flag, 0, sizeof(int), s));
         if (h->dtype == SPMM_HIP_F64)
-            gather_values_kernel<double><<<nb, WG, 0, s>>>((const double *)h->d_val, perm, (double *)dst, n);
+            gather_values_kernel<double><<<nb, WG, 0, s>>>((const double *)h->d_val, perm, (double *)dst, n, flag);
         else
-            gather_values_kernel<float><<<nb, WG, 0, s>>>((const float *)h->d_val, perm, (float *)dst, n);
+            gather_values_kernel<float><<<nb, WG, 0, s>>>((const float *)h->d_val, perm, (float *)dst, n, flag);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? SPMM_HIP_OK : fail(SPMM_HIP_ERR_HIP, std::string("gather launch: ") + hipGetErrorString(e));
     };
-    if (int st = gather(h->d_wperm, h->d_wval, h->nwperm)) return st;
-    if (int st = gather(h->d_tperm, h->d_tval, h->ntperm)) return st;
+    if (int st = gather(h->d_wperm, h->d_wval, h->nwperm, nullptr)) return st;
+    if (int st = gather(h->d_tperm, h->d_tval, h->ntperm, h->plan.tile_mfma ? h->d_mflag : nullptr)) return st;
     return SPMM_HIP_OK;
 }
 }  // namespace
@@ -2182,8 +2220,8 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     return SPMM_HIP_OK;
 }
 
-int spmm_hip_debug_gate(int64_t nnz, int32_t k, int32_t kw, const double *sample, double *out) {
-    if (!sample || !out || nnz < 0 || k < 1 || kw < 1) return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
+int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, const double *sample, double *out) {
+    if (!sample || !out || m < 0 || nnz < 0 || k < 1 || kw < 1) return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
     MfmaGate g;
     g.sampled = (int)sample[0];
     g.r16 = sample[1];
@@ -2192,7 +2230,7 @@ int spmm_hip_debug_gate(int64_t nnz, int32_t k, int32_t kw, const double *sample
     g.tile_nnz = sample[4];
     g.chunks = sample[5];
     g.max_chunks = sample[6];
-    mfma_cost(g, nnz, k, kw);
+    mfma_cost(g, m, nnz, k, kw);
     out[0] = g.verdict;
     out[1] = g.t_on;
     out[2] = g.t_off;

@@ -114,6 +114,7 @@ struct spmm_hip_handle {
     long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
     int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)
     int32_t *d_tperm = nullptr;      // tile chunk-major position -> nonzero, -1 = padding (value updates re-gather tval)
+    int *d_mflag = nullptr;          // matrix-core tiles: {A, B} operand outside the exact range (spmm_mfma.hpp)
     int64_t nwperm = 0, ntperm = 0;
 
     // per-k buffers

@@ -21,24 +21,24 @@
 // tests/test_gpu_mfma.py), so a tile row is the reference's left-to-right
 // chain over its own columns with extra fma(0, b, acc) steps for the panel's empty cells.  Those extra steps are
 // exact no-ops -- and the result does not depend on how the matrix cores treat subnormals -- whenever every nonzero
-// operand the tile's MFMAs see (panel values a, B operand values b) has |x| >= 2^-458 (fp32: 2^-40, the same
-// argument with 24-bit significands and a 2^-126 normal floor) and the chain stays finite (fp64 figures below):
+// operand has 2^-458 <= |x| < 2^500 (fp32: 2^-40 <= |x| < 2^58, the same argument with 24-bit significands and a
+// 2^-126 normal floor; fp64 figures below):
 //   * the chain starts at +0; a product is then 0 (an empty cell or a zero value: acc + (+-0) == acc, and +0 stays
 //     +0) or at least 2^-916 in magnitude with its last bit >= 2^-1020; a step a*b + acc either cancels exactly
 //     (+0, as in the reference) or lands at >= 2^-1021 in magnitude (|acc| near |a*b| has its last bit >= 2^-969,
 //     otherwise one term dominates) -- so no step underflows or produces a subnormal, no -0 ever appears, and an
 //     empty cell never meets a -0 accumulator (fma(+0, b, -0) would give +0 where the reference keeps -0);
-//   * Inf / NaN in B (a panel zero times it makes a NaN the reference does not have) and overflow leave a
-//     non-finite accumulator, which stays non-finite to the chunk's end.
-// A wave checks both after every chunk (the smallest frexp exponent it fed to the MFMAs, the finiteness of its
-// accumulators); on a failure -- adversarial data only -- it recomputes its whole tile by the sparse chain over the
-// real entries with IEEE FMAs (exactly the reference's operations), from +0.  Rows with a repeated column
-// (duplicate .mtx entries) never reach this kernel (the inspector keeps them out).
+//   * no product reaches 2^1000 and no row of <= 2048 of them overflows, and Inf / NaN (a panel zero times them
+//     makes a NaN the reference does not have) are outside the range.
+// The range is checked outside the MFMA loop: A's values when the plan is built and whenever they are updated
+// (mflag[0]), B by mfma_range_kernel before each launch (mflag[1]).  When either is set -- adversarial data only --
+// every wave computes its tile by the sparse chain over the real entries with IEEE FMAs from +0, exactly the
+// reference's operations.  Rows with a repeated column (duplicate .mtx entries) never reach this kernel.
 //
 // Per-wave pipeline, chunk c: A(c) from the panel into VGPRs; clear chunk c's cells, scatter chunk c+1's entries
-// (loaded during chunk c-1); issue the entry loads of chunk c+2; the MFMAs of chunk c (operands range-checked), each
+// (loaded during chunk c-1); issue the entry loads of chunk c+2; the MFMAs of chunk c, each
 // k step's B registers reloaded with chunk c+1's operand as soon as its MFMAs have issued; the union-column loads of
-// chunk c+2; the exact-range ballot.
+// chunk c+2.
 //
 // Tables (inspector build_tiles with 16-row tiles; spmm_engine.hip):
 //   tiles[t]   = {first C row, rows (<= 16), first chunk, chunks}
@@ -71,7 +71,7 @@ template <typename T> struct MfmaT;
 template <> struct MfmaT<double> {
     typedef f64x4 acc_t;
     typedef i32x4 bop_t;
-    static constexpr int MIN_EXP = -457;
+    static constexpr int MIN_EXP = -457, MAX_EXP = 500;
     __device__ static int fexp(double x) { return __builtin_amdgcn_frexp_exp(x); }
     __device__ static acc_t mfma(double a, double b, acc_t c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
     __device__ static bop_t load(__amdgpu_buffer_rsrc_t rs, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0); }
@@ -85,7 +85,7 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 template <> struct MfmaT<float> {
     typedef f32x4 acc_t;
     typedef i32x2 bop_t;
-    static constexpr int MIN_EXP = -39;
+    static constexpr int MIN_EXP = -39, MAX_EXP = 58;
     __device__ static int fexp(float x) { return __builtin_amdgcn_frexp_expf(x); }
     __device__ static acc_t mfma(float a, float b, acc_t c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
     __device__ static bop_t load(__amdgpu_buffer_rsrc_t rs, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0); }
@@ -95,12 +95,13 @@ template <> struct MfmaT<float> {
     __device__ static float fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 };
 
-// CHECK = false: no exact-range check (measurement only: SPMM_HIP_MFMA_CHECK=0 prices the check; never a product path)
-template <typename T, bool XCD, int NP, bool CHECK = true>
+// mflag[0] | mflag[1] != 0: an operand of this run lies outside the exact range (A values: checked at plan time and
+// by every value update; B: mfma_range_kernel before this launch) -- every tile then takes the sparse IEEE chain
+template <typename T, bool XCD, int NP>
 __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm_mfma_tile_kernel(
     const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
     const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, uint32_t b_bytes,
-    T *__restrict__ C, int ld) {
+    T *__restrict__ C, int ld, const int *__restrict__ mflag) {
     using M = MfmaT<T>;
     typedef typename M::acc_t acc_t;
     typedef typename M::bop_t bop_t;
@@ -200,49 +201,35 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
     scatter();
     load_e(min(1, tl.w - 1));
     load_tcol(min(1, tl.w - 1));
-    int emin = 0;          // smallest frexp exponent of an operand this lane fed to the MFMAs
-    bool bad = false;
-    for (int c = 0; c < tl.w; ++c) {
-        const int ns = (tchunk[tl.z + c].y + 3) >> 2;
-        T a[MFMA_KS];
-        const T *pa = P + (l & 15) * MFMA_PST + g;
-#pragma unroll
-        for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
-#pragma unroll
-        for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
-        if (c + 1 < tl.w) scatter();
-        load_e(min(c + 2, tl.w - 1));
-#pragma unroll
-        for (int st = 0; st < MFMA_KS; ++st) {
-            if (st < ns) {
-                if constexpr (CHECK) emin = min(emin, M::fexp(a[st]));
-#pragma unroll
-                for (int p = 0; p < NP; ++p) {
-                    T bb[2];
-                    __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
-                    if constexpr (CHECK) emin = min(emin, min(M::fexp(bb[0]), M::fexp(bb[1])));
-                    acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
-                    acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
-                }
-            }
-            load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
-        }
-        // an operand below the range, or a non-finite accumulator (Inf/NaN in B -- a panel zero times it is NaN --,
-        // or an overflow): the tile goes to the sparse chain
-        if constexpr (CHECK) {
-            bad = emin < M::MIN_EXP;
-#pragma unroll
-            for (int p = 0; p < NP; ++p)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) bad |= !__builtin_isfinite(acc[p][0][i]) || !__builtin_isfinite(acc[p][1][i]);
-            if (__builtin_amdgcn_ballot_w64(bad)) break;
-        }
-        load_tcol(min(c + 2, tl.w - 1));
-    }
-    if (__builtin_amdgcn_ballot_w64(bad)) {      // outside the exact range: the whole tile by the sparse chain
-#pragma unroll
-        for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = acc_t{T(0), T(0), T(0), T(0)};
+    if (__builtin_amdgcn_readfirstlane(mflag[0] | mflag[1]) != 0) {
+        // outside the exact range: the whole tile by the sparse chain from +0 (the reference's operations)
         for (int c = 0; c < tl.w; ++c) sparse_chunk(c);
+    } else {
+        for (int c = 0; c < tl.w; ++c) {
+            const int ns = (tchunk[tl.z + c].y + 3) >> 2;
+            T a[MFMA_KS];
+            const T *pa = P + (l & 15) * MFMA_PST + g;
+#pragma unroll
+            for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
+#pragma unroll
+            for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
+            if (c + 1 < tl.w) scatter();
+            load_e(min(c + 2, tl.w - 1));
+#pragma unroll
+            for (int st = 0; st < MFMA_KS; ++st) {
+                if (st < ns) {
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        T bb[2];
+                        __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
+                        acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
+                        acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
+                    }
+                }
+                load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
+            }
+            load_tcol(min(c + 2, tl.w - 1));
+        }
     }
     const int c0 = 2 * (l & 15);
 #pragma unroll
@@ -257,6 +244,32 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
             }
         }
     }
+}
+
+// Exact-range check of B for the matrix-core tiles (spmm_mfma_tile_kernel's mflag[1]): any value with a frexp
+// exponent outside [MIN_EXP, MAX_EXP] other than +-0 -- subnormals, tiny or huge values, Inf, NaN (frexp gives NaN /
+// Inf the exponent 0, so those are caught by the finiteness test) -- sets *flag.  16-byte loads over n values.
+template <typename T>
+__global__ __launch_bounds__(256) void mfma_range_kernel(const T *__restrict__ B, int64_t n, int *__restrict__ flag) {
+    using M = MfmaT<T>;
+    constexpr int V = 16 / (int)sizeof(T);
+    typedef T tv __attribute__((ext_vector_type(V)));
+    bool bad = false;
+    const int64_t nv = n / V, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+        const tv v = __builtin_nontemporal_load(reinterpret_cast<const tv *>(B) + i);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int e = M::fexp(v[j]);
+            bad |= (v[j] != T(0) && (e < M::MIN_EXP || e > M::MAX_EXP)) || !__builtin_isfinite(v[j]);
+        }
+    }
+    for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const T x = B[i];
+        const int e = M::fexp(x);
+        bad |= (x != T(0) && (e < M::MIN_EXP || e > M::MAX_EXP)) || !__builtin_isfinite(x);
+    }
+    if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 }  // namespace spmm

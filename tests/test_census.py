@@ -84,5 +84,5 @@ def test_debug_gate_reproduces_plan_verdict(S, line):
     A = S.generate(S.gen_params(line))
     for k in (32, 64, 128):
         d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, gate_only=True)
-        g = S.debug_gate(A.nnz, k, d)
+        g = S.debug_gate(A.m, A.nnz, k, d)
         assert g["gate"] == d["gate"] and g["t_on_us"] == d["t_on_us"] and g["t_off_us"] == d["t_off_us"]

@@ -72,17 +72,25 @@ def features(args):
 
 
 def model(F, c):
-    """t_on, t_off (us) for feature rows F with constants c (mirrors mfma_cost)."""
+    """t_on, t_off (us) for feature rows F with constants c (mirrors mfma_cost in spmm_engine.hip)."""
     P = F["k"] / 32.0
     r_row = c["row_us_nnz"] * np.maximum(F["r16"], 1.0) ** -c["row_reuse_exp"] * (F["kw"] / 32.0) ** -c["row_kw_exp"]
-    t_off = c["launch"] + F["nnz"] * P * r_row
-    t_tiles = c["launch"] + P * np.maximum(F["est_chunks"] * c["us_chunk"] + F["est_tiles"] * c["us_tile"],
-                                           F["max_chunks"] * c["us_chain"])
-    t_left = c["launch"] + (F["nnz"] - F["est_tile_nnz"]) * P * r_row
+    t_off = c["launch"] + P * (F["nnz"] * r_row + F["m"] * c["row_us_row"])
+    t_tiles = c["mfma_launch"] + P * np.maximum(F["est_chunks"] * c["us_chunk"] + F["est_tiles"] * c["us_tile"],
+                                                F["max_chunks"] * c["us_chain"])
+    left_rows = np.maximum(F["m"] - 16.0 * F["est_tiles"], 0.0)
+    t_left = c["launch"] + P * ((F["nnz"] - F["est_tile_nnz"]) * r_row + left_rows * c["row_us_row"])
     return np.maximum(t_tiles, t_left), t_off
 
 
+def decide(F, c):
+    """The gate: tiles hold at least MIN_TILE_FRAC of the nonzeros and the model's gain reaches c["gain"]."""
+    m_on, m_off = model(F, c)
+    return (F["est_tile_nnz"] >= c["min_tile_frac"] * F["nnz"]) & (F["est_tiles"] > 0) & (m_off >= c["gain"] * m_on)
+
+
 def fit(args):
+    from scipy.optimize import least_squares
     ab = load_ab(args.ab)
     feats = {}
     for l in open(args.features):
@@ -90,39 +98,43 @@ def fit(args):
         feats[(d["gen"], d["k"])] = d
     keys = [k for k in ab if k in feats and ab[k]["tile_mode"] == "mfma"]
     F = {f: np.array([feats[k][f] if f in feats[k] else ab[k][f] for k in keys], float)
-         for f in ("k", "nnz", "est_chunks", "est_tiles", "est_tile_nnz", "max_chunks", "r16", "kw")}
+         for f in ("k", "nnz", "m", "est_chunks", "est_tiles", "est_tile_nnz", "max_chunks", "r16", "kw")}
     t_on = np.array([ab[k]["ms"] * 1e3 for k in keys])
     t_off = np.array([ab[k]["ms_base"] * 1e3 for k in keys])
-    P = F["k"] / 32.0
-    from scipy.optimize import least_squares
-    # row kernel: t_off = launch + r * nnz * P (relative error)
-    def res_off(x):
-        c = {"launch": x[0], "row_us_nnz": x[1], "row_reuse_exp": x[2], "row_kw_exp": x[3], "us_chunk": 1.0,
-             "us_tile": 0.0, "us_chain": 0.0}
-        return np.log(model(F, c)[1] / t_off)
-    r0 = least_squares(res_off, [10.0, 12e-6, 0.1, 0.1], bounds=([0, 0, -1, -1], [100, 1e-3, 2, 2])).x
-    # the shipped time: max(tile kernel, leftover rows) with the tile kernel's launch + max(throughput, chain)
-    def res_on(x):
-        c = {"launch": r0[0], "row_us_nnz": r0[1], "row_reuse_exp": r0[2], "row_kw_exp": r0[3], "us_chunk": x[0],
-             "us_tile": x[1], "us_chain": x[2]}
-        m_on, _ = model(F, c)
-        return np.log(m_on / t_on)
-    x = least_squares(res_on, [1.6e-3, 1e-3, 4.5], bounds=([0, 0, 0], [1e-2, 1e-2, 50]), loss="soft_l1").x
-    c = {"launch": float(r0[0]), "row_us_nnz": float(r0[1]), "row_reuse_exp": float(r0[2]),
-         "row_kw_exp": float(r0[3]), "us_chunk": float(x[0]), "us_tile": float(x[1]), "us_chain": float(x[2])}
+    base = {"min_tile_frac": 0.0, "gain": 1.0}
+
+    def c_of(x, y):
+        return {**base, "launch": y[0], "row_us_nnz": y[1], "row_reuse_exp": y[2], "row_kw_exp": y[3],
+                "row_us_row": y[4], "mfma_launch": x[0], "us_chunk": x[1], "us_tile": x[2], "us_chain": x[3]}
+    # the row kernel (every line: the baseline plan has no matrix-core tiles)
+    y = least_squares(lambda y: np.log(model(F, c_of([0, 0, 0, 0], y))[1] / t_off), [5, 2.5e-5, 0.2, 0.15, 1e-4],
+                      bounds=([0, 0, -2, -2, 0], [100, 1e-3, 3, 3, 1e-2])).x
+    # the tile kernel on the lines whose tiles hold >= 90 % of the nonzeros (t_on is then the tile kernel)
+    sel = F["est_tile_nnz"] >= 0.9 * F["nnz"]
+    Fs = {k: v[sel] for k, v in F.items()}
+    x = least_squares(lambda x: np.log(model(Fs, c_of(x, y))[0] / t_on[sel]), [20, 1.6e-3, 1.5e-3, 1.1],
+                      bounds=([0, 0, 0, 0], [200, 1e-2, 1e-2, 50]), loss="soft_l1").x
+    c = c_of(x, y)
     m_on, m_off = model(F, c)
-    print(json.dumps({"fit": c, "lines": len(keys),
-                      "rms_log_err_on": float(np.sqrt(np.mean(np.log(m_on / t_on) ** 2))),
+    print(json.dumps({"fit": {k: float(v) for k, v in c.items()}, "lines": len(keys), "tile_lines": int(sel.sum()),
+                      "rms_log_err_on_tile_lines": float(np.sqrt(np.mean(np.log(m_on[sel] / t_on[sel]) ** 2))),
                       "rms_log_err_off": float(np.sqrt(np.mean(np.log(m_off / t_off) ** 2)))}))
-    m_on, m_off = model(F, c)
     sp = t_off / t_on
-    pred = m_off / m_on
-    for thr in (1.0, 1.05, 1.1, 1.15, 1.2, 1.3):
-        on = pred >= thr
-        tot_off, tot_chosen = t_off.sum(), np.where(on, t_on, t_off).sum()
-        print(json.dumps({"gain_threshold": thr, "taken": int(on.sum()), "worst_taken": float(sp[on].min()) if on.any() else None,
-                          "taken_below_0.9": int((sp[on] < 0.9).sum()), "taken_below_1.0": int((sp[on] < 1.0).sum()),
-                          "missed_above_1.1": int((sp[~on] > 1.1).sum()), "aggregate_speedup": round(tot_off / tot_chosen, 4)}))
+    cls = [(k[1], k[0].split()[2], k[0].split()[9]) for k in keys]
+    for frac in (0.0, 0.8, 0.9):
+        for thr in (1.1, 1.2, 1.3, 1.4):
+            cc = {**c, "min_tile_frac": frac, "gain": thr}
+            on = decide(F, cc)
+            chosen = np.where(on, t_on, t_off)
+            worst_cls = min((t_off[[i for i in range(len(keys)) if cls[i] == q and on[i]]].sum() /
+                             t_on[[i for i in range(len(keys)) if cls[i] == q and on[i]]].sum(), q)
+                            for q in set(cls) if any(on[i] for i in range(len(keys)) if cls[i] == q))
+            print(json.dumps({"min_tile_frac": frac, "gain": thr, "taken": int(on.sum()),
+                              "worst_line": round(float(sp[on].min()), 3) if on.any() else None,
+                              "below_0.9": int((sp[on] < 0.9).sum()), "below_1.0": int((sp[on] < 1.0).sum()),
+                              "missed_above_1.2": int((sp[~on] > 1.2).sum()),
+                              "worst_class_taken": [round(float(worst_cls[0]), 3), worst_cls[1]],
+                              "aggregate": round(float(t_off.sum() / chosen.sum()), 4)}))
 
 
 def main():

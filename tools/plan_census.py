@@ -62,7 +62,7 @@ def regate(args):
     pairs = []
     with open(args.regate_out, "w") as f:
         for r in recs:
-            g = S.debug_gate(r["nnz"], r["k"], r)
+            g = S.debug_gate(r["m"], r["nnz"], r["k"], r)
             r.update({"gate": g["gate"], "t_on_us": round(g["t_on_us"], 5), "t_off_us": round(g["t_off_us"], 5),
                       "mode": "mfma" if g["gate"] else "none", "engine_sha256": sha, "sampled_by": r["engine_sha256"]})
             f.write(json.dumps(r) + "\n")
