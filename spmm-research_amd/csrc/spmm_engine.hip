@@ -287,28 +287,20 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
     }
 }
 
-// Matrix-core tiles over columns [k0, k0 + kw) (kw a multiple of 32): four 16-row tiles (one per wave) per
-// workgroup; a wave owns 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (DESIGN §6.18;
-// SPMM_HIP_MFMA_NP=1 keeps 32).  B and C point at column k0; the buffer descriptor of B covers the rest of the array.
+// Matrix-core tiles over all K columns (a multiple of 32): four 16-row tiles (one per wave) per workgroup; a wave owns
+// 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (SPMM_HIP_MFMA_NP=1 keeps
+// 32).  The buffer descriptor of B covers the rest of the array from the sub-panel on.
 template <typename T>
-void launch_mfma(spmm_hip_t *h, const T *B, T *C, int ld, int k0, int kw, hipStream_t s) {
+void launch_mfma(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
     const int np_max = env_int("SPMM_HIP_MFMA_NP", 2) >= 2 ? 2 : 1;
-    // B's exact-range check (spmm_mfma.hpp) into mflag[1], on the tiles' stream before their launch
-    {
-        const int64_t n = (int64_t)h->ncols * ld - k0;
-        const int64_t nv = (n + 16 / (int64_t)sizeof(T) - 1) / (16 / (int64_t)sizeof(T));
-        const unsigned rg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, (nv + WG - 1) / WG));
-        (void)hipMemsetAsync(h->d_mflag + 1, 0, sizeof(int), s);
-        mfma_range_kernel<T><<<rg, WG, 0, s>>>(B, n, h->d_mflag + 1);
-    }
-    for (int k1 = 0; k1 + 32 <= kw;) {
-        const int np = (np_max >= 2 && k1 + 64 <= kw) ? 2 : 1;
-        const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)ld - (size_t)(k0 + k1)) * sizeof(T));
+    for (int k1 = 0; k1 + 32 <= K;) {
+        const int np = (np_max >= 2 && k1 + 64 <= K) ? 2 : 1;
+        const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)K - (size_t)k1) * sizeof(T));
         auto go = [&](auto xcd_c, auto np_c) {
             spmm_mfma_tile_kernel<T, decltype(xcd_c)::value, decltype(np_c)::value><<<grid, WG, 0, s>>>(
                 h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const T *)h->d_tval, h->d_tlidx, B + k1, bb,
-                C + k1, ld, h->d_mflag);
+                C + k1, K);
         };
         using N1 = std::integral_constant<int, 1>;
         using N2 = std::integral_constant<int, 2>;
@@ -318,13 +310,38 @@ void launch_mfma(spmm_hip_t *h, const T *B, T *C, int ld, int k0, int kw, hipStr
     }
 }
 
+// The matrix-core tiles' exact range (spmm_mfma.hpp): B's check, on the row kernel's stream (beside the tiles when
+// that is the side stream) -- an out-of-range B stores this launch's sequence number into mflag[1] (no reset launch;
+// a stale number of an earlier launch never matches, and under a graph replay a baked-in number can only keep the
+// exact fallback on, never skip it) ...
+template <typename T>
+int launch_mfma_check(spmm_hip_t *h, const T *B, int K, hipStream_t rs) {
+    h->mflag_seq = h->mflag_seq == INT32_MAX ? 1 : h->mflag_seq + 1;
+    const int64_t n = (int64_t)h->ncols * K;
+    const int64_t nv = (n + 16 / (int64_t)sizeof(T) - 1) / (16 / (int64_t)sizeof(T));
+    const unsigned rg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, (nv + WG - 1) / WG));
+    mfma_range_kernel<T><<<rg, WG, 0, rs>>>(B, n, h->d_mflag + 1, h->mflag_seq);
+    return h->mflag_seq;
+}
+
+// ... and after the tiles and the check (the join): every tile recomputed by the sparse IEEE chain when A or B is out
+// of range, else an immediate exit
+template <typename T>
+void launch_mfma_fixup(spmm_hip_t *h, const T *B, T *C, int K, int seq, hipStream_t s) {
+    const int grid = std::min((h->plan.ntile + 3) / 4, 512);
+    mfma_fixup_kernel<T><<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const T *)h->d_tval,
+                                             h->d_tlidx, B, C, K, K, h->d_mflag, seq);
+}
+
 // rs: the stream of the row kernel and the combine (the launch stream, or the handle's side stream when the row kernel
 // only runs the leftover rows of a matrix-core plan, concurrently with the tiles on s)
 template <typename T>
-void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStream_t rs) {
+void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStream_t rs, int *seq) {
     T *P = (T *)h->d_part;
+    const bool mf = h->plan.ntile > 0 && h->plan.tile_mfma;
+    if (mf) *seq = launch_mfma_check<T>(h, B, K, rs);
     // matrix-core tiles: one pass over all K columns (the row kernel's K panels are for its B gather, not theirs)
-    if (h->plan.ntile > 0 && h->plan.tile_mfma) launch_mfma<T>(h, B, C, K, 0, K, s);
+    if (mf) launch_mfma<T>(h, B, C, K, s);
     for (int p = 0; p < h->plan.npanels; ++p) {
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
@@ -338,20 +355,28 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStr
 }
 
 int launch_spmm(spmm_hip_t *h, const void *B, void *C, int K, hipStream_t s) {
-    // matrix-core plans: the leftover rows (a skewed row's pieces, low-reuse tiles) run beside the tile kernel
-    const bool par = h->plan.tile_mfma && h->plan.ntile > 0 && h->nblk > 0 && h->side;
+    // matrix-core plans: the exact-range check of B and the leftover rows (a skewed row's pieces, low-reuse tiles) run
+    // beside the tile kernel; the fix-up follows the join
+    const bool mf = h->plan.tile_mfma && h->plan.ntile > 0;
+    const bool par = mf && h->side;
     if (par) {
         HIPCHK(hipEventRecord(h->ev_fork, s));
         HIPCHK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
     }
     hipStream_t rs = par ? h->side : s;
-    if (h->dtype == SPMM_HIP_F64)
-        launch_spmm_t<double>(h, (const double *)B, (double *)C, K, s, rs);
+    int seq = 0;
+    const bool f64 = h->dtype == SPMM_HIP_F64;
+    if (f64)
+        launch_spmm_t<double>(h, (const double *)B, (double *)C, K, s, rs, &seq);
     else
-        launch_spmm_t<float>(h, (const float *)B, (float *)C, K, s, rs);
+        launch_spmm_t<float>(h, (const float *)B, (float *)C, K, s, rs, &seq);
     if (par) {
         HIPCHK(hipEventRecord(h->ev_join, h->side));
         HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
+    }
+    if (mf) {
+        if (f64) launch_mfma_fixup<double>(h, (const double *)B, (double *)C, K, seq, s);
+        else launch_mfma_fixup<float>(h, (const float *)B, (float *)C, K, seq, s);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SPMM_HIP_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
@@ -1726,7 +1751,7 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
                          tp.tseg.size() * 2 + tp.tlidx.size() * 2 + tval.size();
     }
     // the side stream of matrix-core plans (created here, never inside a run: runs may be graph-captured)
-    if (e == hipSuccess && h->plan.tile_mfma && h->nblk > 0 && !h->side) {
+    if (e == hipSuccess && h->plan.tile_mfma && !h->side) {
         e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);

@@ -115,6 +115,7 @@ struct spmm_hip_handle {
     int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)
     int32_t *d_tperm = nullptr;      // tile chunk-major position -> nonzero, -1 = padding (value updates re-gather tval)
     int *d_mflag = nullptr;          // matrix-core tiles: {A, B} operand outside the exact range (spmm_mfma.hpp)
+    int mflag_seq = 0;               // matrix-core launches so far: mflag[1] == seq marks THIS launch's B as out of range
     int64_t nwperm = 0, ntperm = 0;
 
     // per-k buffers

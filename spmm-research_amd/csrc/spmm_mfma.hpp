@@ -31,9 +31,10 @@
 //   * no product reaches 2^1000 and no row of <= 2048 of them overflows, and Inf / NaN (a panel zero times them
 //     makes a NaN the reference does not have) are outside the range.
 // The range is checked outside the MFMA loop: A's values when the plan is built and whenever they are updated
-// (mflag[0]), B by mfma_range_kernel before each launch (mflag[1]).  When either is set -- adversarial data only --
-// every wave computes its tile by the sparse chain over the real entries with IEEE FMAs from +0, exactly the
-// reference's operations.  Rows with a repeated column (duplicate .mtx entries) never reach this kernel.
+// (mflag[0]), B by mfma_range_kernel on the side stream beside the tile kernel (mflag[1] == the launch's sequence
+// number).  When either is set -- adversarial data only -- mfma_fixup_kernel, after both, recomputes every tile by
+// the sparse chain over the real entries with IEEE FMAs from +0, exactly the reference's operations.  Rows with a
+// repeated column (duplicate .mtx entries) never reach this kernel.
 //
 // Per-wave pipeline, chunk c: A(c) from the panel into VGPRs; clear chunk c's cells, scatter chunk c+1's entries
 // (loaded during chunk c-1); issue the entry loads of chunk c+2; the MFMAs of chunk c, each
@@ -95,13 +96,12 @@ template <> struct MfmaT<float> {
     __device__ static float fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 };
 
-// mflag[0] | mflag[1] != 0: an operand of this run lies outside the exact range (A values: checked at plan time and
-// by every value update; B: mfma_range_kernel before this launch) -- every tile then takes the sparse IEEE chain
+// No range check here: mfma_fixup_kernel recomputes every tile when an operand lies outside the exact range
 template <typename T, bool XCD, int NP>
 __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm_mfma_tile_kernel(
     const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
     const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, uint32_t b_bytes,
-    T *__restrict__ C, int ld, const int *__restrict__ mflag) {
+    T *__restrict__ C, int ld) {
     using M = MfmaT<T>;
     typedef typename M::acc_t acc_t;
     typedef typename M::bop_t bop_t;
@@ -157,42 +157,6 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
             hc[j] = cell;
         }
     };
-    // chunk c by the sparse chain (IEEE FMAs over the chunk's real entries in order, from the accumulators): an
-    // entry of row r updates this lane's outputs when the lane owns row r (the fallback of a tile with an operand
-    // outside the exact range)
-    auto sparse_chunk = [&](int c) {
-        const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
-        T x[NP][8];
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) x[p][i] = acc[p][0][i], x[p][4 + i] = acc[p][1][i];
-#pragma unroll 1
-        for (int e = ch.z; e < cn.z; ++e) {
-            const int cell = (int)tpos[e];
-            const int r = cell / MFMA_PST, k = cell % MFMA_PST;
-            if (cell == MFMA_TRASH || !M::owns(r, g)) continue;
-            const int row = tcolT[(size_t)(tl.z + c) * MFMA_UC + (k & 3) * MFMA_KS + (k >> 2)];
-            const T av = tval[e];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) {
-                const bop_t v = M::load(rs, (uint32_t)row * ldb + lane_off + SUB * p);
-                T bb[2];
-                __builtin_memcpy(bb, &v, 2 * sizeof(T));
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (q == M::slot(r)) {
-                        x[p][q] = M::fma(av, bb[0], x[p][q]);
-                        x[p][4 + q] = M::fma(av, bb[1], x[p][4 + q]);
-                    }
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[p][0][i] = x[p][i], acc[p][1][i] = x[p][4 + i];
-    };
-
     // prologue: chunk 0 in the panel, B operand of chunk 0, entries and union columns of chunk 1
     load_tcol(0);
 #pragma unroll
@@ -201,35 +165,30 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
     scatter();
     load_e(min(1, tl.w - 1));
     load_tcol(min(1, tl.w - 1));
-    if (__builtin_amdgcn_readfirstlane(mflag[0] | mflag[1]) != 0) {
-        // outside the exact range: the whole tile by the sparse chain from +0 (the reference's operations)
-        for (int c = 0; c < tl.w; ++c) sparse_chunk(c);
-    } else {
-        for (int c = 0; c < tl.w; ++c) {
-            const int ns = (tchunk[tl.z + c].y + 3) >> 2;
-            T a[MFMA_KS];
-            const T *pa = P + (l & 15) * MFMA_PST + g;
+    for (int c = 0; c < tl.w; ++c) {
+        const int ns = (tchunk[tl.z + c].y + 3) >> 2;
+        T a[MFMA_KS];
+        const T *pa = P + (l & 15) * MFMA_PST + g;
 #pragma unroll
-            for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
+        for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
 #pragma unroll
-            for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
-            if (c + 1 < tl.w) scatter();
-            load_e(min(c + 2, tl.w - 1));
+        for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
+        if (c + 1 < tl.w) scatter();
+        load_e(min(c + 2, tl.w - 1));
 #pragma unroll
-            for (int st = 0; st < MFMA_KS; ++st) {
-                if (st < ns) {
+        for (int st = 0; st < MFMA_KS; ++st) {
+            if (st < ns) {
 #pragma unroll
-                    for (int p = 0; p < NP; ++p) {
-                        T bb[2];
-                        __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
-                        acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
-                        acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
-                    }
+                for (int p = 0; p < NP; ++p) {
+                    T bb[2];
+                    __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
+                    acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
+                    acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
                 }
-                load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
             }
-            load_tcol(min(c + 2, tl.w - 1));
+            load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
         }
+        load_tcol(min(c + 2, tl.w - 1));
     }
     const int c0 = 2 * (l & 15);
 #pragma unroll
@@ -246,18 +205,20 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
     }
 }
 
-// Exact-range check of B for the matrix-core tiles (spmm_mfma_tile_kernel's mflag[1]): any value with a frexp
-// exponent outside [MIN_EXP, MAX_EXP] other than +-0 -- subnormals, tiny or huge values, Inf, NaN (frexp gives NaN /
-// Inf the exponent 0, so those are caught by the finiteness test) -- sets *flag.  16-byte loads over n values.
+// Exact-range check of B for the matrix-core tiles (mflag[1]; on the side stream beside the tile kernel): any value
+// with a frexp exponent outside [MIN_EXP, MAX_EXP] other than +-0 -- subnormals, tiny or huge values, Inf, NaN
+// (frexp gives NaN / Inf the exponent 0, so those are caught by the finiteness test) -- stores seq into *flag.
+// 16-byte loads over n values.
 template <typename T>
-__global__ __launch_bounds__(256) void mfma_range_kernel(const T *__restrict__ B, int64_t n, int *__restrict__ flag) {
+__global__ __launch_bounds__(256) void mfma_range_kernel(const T *__restrict__ B, int64_t n, int *__restrict__ flag,
+                                                         int seq) {
     using M = MfmaT<T>;
     constexpr int V = 16 / (int)sizeof(T);
     typedef T tv __attribute__((ext_vector_type(V)));
     bool bad = false;
     const int64_t nv = n / V, stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
-        const tv v = __builtin_nontemporal_load(reinterpret_cast<const tv *>(B) + i);
+        const tv v = reinterpret_cast<const tv *>(B)[i];
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int e = M::fexp(v[j]);
@@ -269,7 +230,57 @@ __global__ __launch_bounds__(256) void mfma_range_kernel(const T *__restrict__ B
         const int e = M::fexp(x);
         bad |= (x != T(0) && (e < M::MIN_EXP || e > M::MAX_EXP)) || !__builtin_isfinite(x);
     }
-    if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+    if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicExch(flag, seq);
+}
+
+// The tiles of a launch with an operand outside the exact range (mflag[0]: A's values, set at plan time or by a value
+// update; mflag[1] == seq: this launch's B, mfma_range_kernel) recomputed after the tile kernel, over all K columns, by
+// the sparse chain over each row's real entries with IEEE FMAs from +0 -- exactly the reference's operations.  Every
+// other launch leaves at its first instruction.  One wave per tile (grid-stride); lane l owns C columns 2j, 2j+1 of
+// each 32-column sub-panel (j = l & 15) for the rows r with M::owns(r, l >> 4), as the tile kernel's accumulators.
+template <typename T>
+__global__ __launch_bounds__(256) void mfma_fixup_kernel(
+    const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
+    const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, T *__restrict__ C, int ld,
+    int K, const int *__restrict__ mflag, int seq) {
+    using M = MfmaT<T>;
+    if (__builtin_amdgcn_readfirstlane(mflag[0] == 0 && mflag[1] != seq)) return;
+    const int l = threadIdx.x % 64, g = l >> 4, c0 = 2 * (l & 15);
+    const int nw = (int)gridDim.x * 4;
+    for (int t = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)threadIdx.x / 64); t < ntiles; t += nw) {
+        const int4 tl = tiles[t];
+        for (int k0 = 0; k0 + 32 <= K; k0 += 32) {
+            T x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = T(0);
+            for (int c = 0; c < tl.w; ++c) {
+                const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
+                for (int e = ch.z; e < cn.z; ++e) {
+                    const int cell = (int)tpos[e];
+                    const int r = cell / MFMA_PST, k = cell % MFMA_PST;
+                    if (cell == MFMA_TRASH || !M::owns(r, g)) continue;
+                    const int row = tcolT[(size_t)(tl.z + c) * MFMA_UC + (k & 3) * MFMA_KS + (k >> 2)];
+                    const T av = tval[e];
+                    const T *b = B + (size_t)row * ld + k0 + c0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (q == M::slot(r)) {
+                            x[q] = M::fma(av, b[0], x[q]);
+                            x[4 + q] = M::fma(av, b[1], x[4 + q]);
+                        }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = M::row(g, i);
+                if (r < tl.y) {
+                    T *p = C + (size_t)(tl.x + r) * ld + k0 + c0;
+                    p[0] = x[i];
+                    p[1] = x[4 + i];
+                }
+            }
+        }
+    }
 }
 
 }  // namespace spmm

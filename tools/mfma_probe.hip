@@ -21,17 +21,11 @@ extern "C" int mfma_probe_launch(int ntiles, const void *tiles, const void *tchu
     auto b = (const double *)B;
     auto c = (double *)C;
     if (b_bytes >= (1ll << 32)) return -2;
-    // the exact-range flags cleared: the probe feeds operands in range (the engine checks them, §3.9)
-    static int *flag = nullptr;
-    if (!flag) {
-        if (hipMalloc(&flag, 2 * sizeof(int)) != hipSuccess) return -3;
-        if (hipMemset(flag, 0, 2 * sizeof(int)) != hipSuccess) return -3;
-    }
     if (xcd & 1)
         spmm_mfma_tile_kernel<double, true, 1><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes,
-                                                                     c, ld, flag);
+                                                                     c, ld);
     else
         spmm_mfma_tile_kernel<double, false, 1><<<grid, 256, 0, st>>>(t, ntiles, ch, tc, tv, tp, b, (uint32_t)b_bytes,
-                                                                      c, ld, flag);
+                                                                      c, ld);
     return (int)hipGetLastError();
 }
