@@ -13,7 +13,9 @@ the plan of the config-3 sweep build b4d29bad); every other line's plan is uncha
 the plan fingerprints on a sample).  tools/sessions/r04_sweep.sh re-measures exactly the changed (line, K) pairs
 (profiles/r04/changed_pairs.txt, written by `--pairs-out`) against the plan without matrix-core tiles.
 
-  python tools/plan_census.py --k 32,128 --workers 6 --out profiles/r04_plan_census.jsonl
+  python tools/plan_census.py --k 32,128 --workers 6 --out /tmp/plan_census.jsonl
+  python tools/plan_census.py --out /tmp/plan_census.jsonl --regate-out profiles/r04/plan_census.jsonl \
+      --pairs-out profiles/r04/changed_pairs.txt        # then gzip: profiles/r04/plan_census.jsonl.gz
 """
 from __future__ import annotations
 

@@ -9,7 +9,7 @@ flags (exact rows of both plans bit-identical; the oracle check of the shipped p
 census of the same build, tools/plan_census.py) it also reports how many of the changed (line, K) pairs the records
 cover.
 
-  python tools/summarize_ab.py profiles/r04/ab_changed*.jsonl.gz --census profiles/r04/plan_census.jsonl
+  python tools/summarize_ab.py profiles/r04/ab_changed*.jsonl.gz --census profiles/r04/plan_census.jsonl.gz
 """
 import argparse
 import gzip
@@ -41,7 +41,8 @@ def main():
     out = []
     if args.census:
         changed = set()
-        for l in open(args.census):
+        op = gzip.open if args.census.endswith(".gz") else open
+        for l in op(args.census, "rt"):
             d = json.loads(l)
             if d.get("mode") == "mfma":
                 changed.add((d["gen"], d["k"]))
