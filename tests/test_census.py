@@ -86,3 +86,18 @@ def test_debug_gate_reproduces_plan_verdict(S, line):
         d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, gate_only=True)
         g = S.debug_gate(A.m, A.nnz, k, d)
         assert g["gate"] == d["gate"] and g["t_on_us"] == d["t_on_us"] and g["t_off_us"] == d["t_off_us"]
+
+
+def test_plan_without_tiles_is_config3_plan():
+    """The plan without matrix-core tiles (SPMM_HIP_MFMA=-1) reproduces the plans the config-3 sweep build recorded
+    (engine b4d29bad, profiles/r03_sweep_medium.jsonl.gz) -- on a sparse stride sample of small lines, all K."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    if not (root / "profiles" / "r03_sweep_medium.jsonl.gz").exists():
+        pytest.skip("config-3 sweep records not present")
+    sys.path.insert(0, str(root / "tools"))
+    import plan_vs_r03
+    res = plan_vs_r03.compare(stride=997, max_nnz=3e6, workers=1)
+    assert len(res) >= 20
+    assert [r for r in res if r[2]] == []
