@@ -176,6 +176,61 @@ def test_mfma_graph_replay(env, monkeypatch):
     mf.close()
 
 
+def test_mfma_range_check_per_launch(env, monkeypatch):
+    """B's exact-range check is per launch: launches alternating in-range and out-of-range B (NaN, a
+    subnormal) on one handle -- each exact row bit-identical to the oracle (NaN where the oracle has NaN), so the
+    fix-up neither sticks after a bad B nor is skipped after a good one; and a captured graph replayed after its B
+    turned in-range and out-of-range again stays exact (a baked-in launch number can only keep the fix-up on)."""
+    torch, S, O = env
+    A = S.generate(S.gen_params(MATS[0]))
+    k = 32
+    mf = handle(S, A, A.values, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    assert mf.tile_info()["mode"] == "mfma"
+    ex = mf.exact_rows()
+    dev = torch.device("cuda", 0)
+    base = O.drand48(11, A.ncols * k).reshape(A.ncols, k) * 2.0 - 1.0
+    cols = np.unique(A.col_idx)
+    bad_nan, bad_sub = base.copy(), base.copy()
+    bad_nan[cols[len(cols) // 2], 3] = np.nan
+    bad_sub[cols[len(cols) // 3], 5] = 2.0 ** -1060
+    want = {}
+    for name, xb in (("ok", base), ("nan", bad_nan), ("sub", bad_sub)):
+        want[name] = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, np.ascontiguousarray(xb.T).reshape(-1), k)
+    B = torch.empty((A.ncols, k), dtype=torch.float64, device=dev)
+    C = torch.empty((A.m, k), dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def check(name):
+        got = C.cpu().numpy()[ex]
+        w = want[name][ex]
+        assert np.array_equal(np.isnan(got), np.isnan(w)), name
+        fin = ~np.isnan(w)
+        assert np.array_equal(bits(got[fin]), bits(w[fin])), name
+
+    src = {"ok": base, "nan": bad_nan, "sub": bad_sub}
+    for name in ("ok", "nan", "ok", "sub", "ok", "ok", "nan", "ok"):
+        B.copy_(torch.from_numpy(src[name]))
+        C.fill_(7.0)
+        mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), k, st.cuda_stream)
+        torch.cuda.synchronize()
+        check(name)
+    s = torch.cuda.Stream(dev)
+    B.copy_(torch.from_numpy(bad_nan))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), k, s.cuda_stream)
+    for name in ("nan", "ok", "sub", "ok"):
+        B.copy_(torch.from_numpy(src[name]))
+        C.fill_(7.0)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        check(name)
+    mf.close()
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # IEEE edge cases (spmm_mfma.hpp header: the exact-chain range check).  The reference sums each row as one chain of
 # fused multiply-adds from +0 in IEEE double on x86 (spmm_kernel_csr.cpp:87-91): subnormal operands and products,
