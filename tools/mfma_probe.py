@@ -81,11 +81,18 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--xcd", type=int, default=1)
     ap.add_argument("--dbg", default="", help="extra kernel variants timed (probe codes: 3 no MFMA, 5 no B loads)")
+    ap.add_argument("--lr-lib", default="", help="also time (and check bit for bit) this probe library on the same "
+                    "tables, e.g. spmm-research_amd/lib/libmfma_probe_lr.so (tools/mfma_lr.hpp)")
+    ap.add_argument("--no-forced", action="store_true", help="skip the engine forced onto the tile plan")
     args = ap.parse_args()
     import torch
     import spmm_amd as S
     L = C.CDLL(str(ROOT / "spmm-research_amd" / "lib" / "libmfma_probe.so"))
     L.mfma_probe_launch.argtypes = [C.c_int] + [C.c_void_p] * 6 + [C.c_longlong, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    LR = None
+    if args.lr_lib:
+        LR = C.CDLL(str(ROOT / args.lr_lib))
+        LR.mfma_probe_launch.argtypes = L.mfma_probe_launch.argtypes
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
@@ -171,6 +178,23 @@ def main():
                 t_m = timed(launch)
                 for v in (int(x) for x in args.dbg.split(",") if x):
                     case[f"dbg{v}_ms"] = round(timed(lambda: launch(v)), 5)
+                if LR is not None:
+                    Cl = torch.zeros_like(C_ref)
+                    lr = lambda xcd=args.xcd: LR.mfma_probe_launch(nt, d_tiles.data_ptr(), d_chunks.data_ptr(),
+                                                                   d_tcol.data_ptr(), d_val.data_ptr(), d_pos.data_ptr(),
+                                                                   B.data_ptr(), bb, Cl.data_ptr(), k, xcd, sp)
+                    assert lr() == 0
+                    torch.cuda.synchronize()
+                    case["lr_same_as_mfma"] = bool(torch.equal(Cl[rows].view(torch.int64), Cm[rows].view(torch.int64)))
+                    case["lr_bitexact"] = bool(torch.equal(Cl[ex].view(torch.int64), C_ref[ex].view(torch.int64)))
+                    case["lr_ms"] = round(timed(lr), 5)
+                    del Cl
+                if args.no_forced:
+                    tile_nnz = int(np.diff(A.row_ptr)[plan["in_tile"]].sum())
+                    case.update({"tile_nnz": tile_nnz, "chunks": int(len(plan["chunks"]) - 1), "mfma_ms": round(t_m, 5)})
+                    out["cases"].append(case)
+                    del d_tiles, d_chunks, d_tcol, d_val, d_pos, Cm
+                    continue
                 os.environ.update({"SPMM_HIP_TILES": "1", "SPMM_HIP_TILE_REUSE": str(reuse),
                                    "SPMM_HIP_TILE_ROWS": str(rmax)})
                 hf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0)
