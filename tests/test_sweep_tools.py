@@ -58,3 +58,31 @@ def test_sweep_where_filter_selects_the_matrix_core_classes():
     full = sweep.dataset_index_lines(a)
     assert len(full) == 16190
     assert [i for i, _ in sel] == [i for i, l in full if float(l.split()[9]) == 0.95 and float(l.split()[2]) >= 20]
+
+
+def test_pmc_busy_time_counts_overlap_once():
+    """tools/pmc_dataset.py: a matrix-core launch overlaps kernels on two streams; its kernel time is the union of
+    the dispatch intervals, not their sum."""
+    import pmc_dataset as P
+    assert P.busy_ns([(0, 10), (5, 20), (30, 40)]) == 30
+    assert P.busy_ns([(0, 100), (10, 20)]) == 100
+    disp = [(1, "spmm_mfma_tile_kernel<double>", {"ns": 100.0}, (0.0, 100.0)),
+            (2, "mfma_range_kernel<double>", {"ns": 20.0}, (5.0, 25.0)),
+            (3, "spmm_rows_kernel<double>", {"ns": 50.0}, (25.0, 75.0)),
+            (4, "mfma_fixup_kernel<double>", {"ns": 4.0}, (104.0, 108.0)),
+            (5, "at::FillFunctor", {"ns": 1.0}, (110.0, 111.0))]
+    g = P.per_matrix(disp, 1)
+    assert g[0]["ns"] == 174.0 and g[0]["busy_ns"] == 104.0
+
+
+def test_sweep_done_pairs_and_changed_pairs(tmp_path):
+    """tools/sweep_done_pairs.py lists the measured (line, K) pairs of A/B record files in the census pair format."""
+    import json
+    import subprocess
+    rec = tmp_path / "r.jsonl"
+    rec.write_text(json.dumps({"gen": "1 1 1", "k": 32, "ms": 1.0, "ms_base": 1.1}) + "\n" +
+                   json.dumps({"gen": "2 2 2", "k": 128, "ms": 1.0}) + "\n")
+    out = tmp_path / "done.txt"
+    tool = Path(__file__).resolve().parents[1] / "tools" / "sweep_done_pairs.py"
+    subprocess.run([sys.executable, str(tool), str(rec), "--out", str(out)], check=True, capture_output=True)
+    assert out.read_text() == "32\t1 1 1\n"
