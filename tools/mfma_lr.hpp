@@ -2,7 +2,8 @@
 // tools/mfma_probe.py --lr-lib.  Against csrc/spmm_mfma.hpp: the A panel is read per k step from LDS and
 // the panel cleared and refilled after the chunk's MFMAs (no 12-value A register array), the whole panel is cleared
 // with 16-byte stores (no remembered cells), and the next chunk's 48 union columns wait in LDS (one VGPR per lane
-// instead of 12).  fp64 NP = 1: 120 VGPRs, 4 waves per SIMD (engine: 154, 3); NP = 2: 184 (218), 2 waves.
+// instead of 12).  fp64 NP = 1: 120 VGPRs, 4 waves per SIMD (engine: 154, 3); NP = 2: 186 (218), 2 waves.  R < 12
+// keeps only R B operands per sub-panel in flight: NP = 1 R = 6 96 VGPRs (5 waves), NP = 2 R = 6 / 8 138 / 152 (3).
 // spmm_mfma.hpp -- gfx950 matrix-core (MFMA) tile kernel of the CSR SpMM engine.
 //
 // The sparse tile kernel (spmm_kernels.hpp, spmm_tile_kernel) reads one staged B row from LDS per nonzero and does
@@ -101,9 +102,13 @@ template <> struct MfmaT<float> {
     __device__ static float fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 };
 
+template <typename T, int NP, int R>
+constexpr int WAVES_LR = sizeof(T) == 4 ? 4 : NP == 1 ? (R <= 6 ? 5 : 4) : (R == MFMA_KS ? 2 : 3);
 // No range check here: mfma_fixup_kernel recomputes every tile when an operand lies outside the exact range
-template <typename T, bool XCD, int NP>
-__global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 4 : 2) void spmm_mfma_tile_kernel(
+// R: B-operand ring slots per sub-panel (R = MFMA_KS: a whole chunk of operands in flight, as the engine; R < MFMA_KS:
+// the operand of step s + R -- of this chunk or the next -- is loaded when step s's MFMAs have issued)
+template <typename T, bool XCD, int NP, int R = MFMA_KS>
+__global__ __launch_bounds__(256, (WAVES_LR<T, NP, R>)) void spmm_mfma_tile_kernel(
     const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
     const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, uint32_t b_bytes,
     T *__restrict__ C, int ld) {
@@ -127,9 +132,9 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 4 : 2) void spmm
     acc_t acc[NP][2];
 #pragma unroll
     for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = acc_t{T(0), T(0), T(0), T(0)};
-    bop_t bo[NP][MFMA_KS];
-    __shared__ int stc[4 * MFMA_UC];          // each wave's union columns of the chunk whose B operand is loading
-    int *TC = stc + wave * MFMA_UC;
+    bop_t bo[NP][R];
+    __shared__ int stc[4 * 2 * MFMA_UC];      // each wave's union columns of chunks c and c+1 (double buffer)
+    int *TCb = stc + wave * 2 * MFMA_UC;
     int tn = 0;                                // this lane's union column of the next chunk (lanes < 48)
     T ev[MFMA_NPE];
     int ep[MFMA_NPE];
@@ -137,13 +142,14 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 4 : 2) void spmm
     auto load_tcol = [&](int c) {                 // chunk c's 48 union columns, one per lane < 48, into tn
         if (l < MFMA_UC) tn = tcolT[(size_t)(tl.z + c) * MFMA_UC + l];
     };
-    auto put_tcol = [&]() {
-        if (l < MFMA_UC) TC[l] = tn;
+    auto put_tcol = [&](int buf) {
+        if (l < MFMA_UC) TCb[buf * MFMA_UC + l] = tn;
     };
-    auto load_b1 = [&](int st) {
-        const int col = TC[g * MFMA_KS + st];
+    // operand of step st of the chunk whose columns sit in buffer buf, into ring slot st % R
+    auto load_b1 = [&](int buf, int st) {
+        const int col = TCb[buf * MFMA_UC + g * MFMA_KS + st];
 #pragma unroll
-        for (int p = 0; p < NP; ++p) bo[p][st] = M::load(rs, (uint32_t)col * ldb + lane_off + SUB * p);
+        for (int p = 0; p < NP; ++p) bo[p][st % R] = M::load(rs, (uint32_t)col * ldb + lane_off + SUB * p);
     };
     auto load_e = [&](int c) {
         const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
@@ -164,16 +170,17 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 4 : 2) void spmm
     };
     // prologue: chunk 0 in the panel, B operand of chunk 0, entries and union columns of chunk 1
     load_tcol(0);
-    put_tcol();
+    put_tcol(0);
 #pragma unroll
-    for (int st = 0; st < MFMA_KS; ++st) load_b1(st);
+    for (int st = 0; st < R; ++st) load_b1(0, st);
     load_e(0);
     scatter();
     load_e(min(1, tl.w - 1));
     load_tcol(min(1, tl.w - 1));
     for (int c = 0; c < tl.w; ++c) {
         const int ns = (tchunk[tl.z + c].y + 3) >> 2;
-        put_tcol();                                // chunk c+1's columns: its B operand loads during these MFMAs
+        const int cur = c & 1, nxt = cur ^ 1;
+        put_tcol(nxt);                             // chunk c+1's columns: its B operand loads during these MFMAs
         const T *pa = P + (l & 15) * MFMA_PST + g;
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) {
@@ -182,12 +189,13 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 4 : 2) void spmm
 #pragma unroll
                 for (int p = 0; p < NP; ++p) {
                     T bb[2];
-                    __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
+                    __builtin_memcpy(bb, &bo[p][st % R], 2 * sizeof(T));
                     acc[p][0] = M::mfma(a, bb[0], acc[p][0]);
                     acc[p][1] = M::mfma(a, bb[1], acc[p][1]);
                 }
             }
-            load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
+            if (st + R < MFMA_KS) load_b1(cur, st + R);     // this chunk's step st + R
+            else load_b1(nxt, st + R - MFMA_KS);            // the next chunk's step st + R - 12
         }
         {   // clear the whole panel (16-byte stores; cheaper in registers than remembering chunk c's cells)
             typedef int i32x4v __attribute__((ext_vector_type(4)));

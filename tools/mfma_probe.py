@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--lr-lib", default="", help="also time (and check bit for bit) this probe library on the same "
                     "tables, e.g. spmm-research_amd/lib/libmfma_probe_lr.so (tools/mfma_lr.hpp)")
     ap.add_argument("--no-forced", action="store_true", help="skip the engine forced onto the tile plan")
+    ap.add_argument("--variants", default="", help="with --lr-lib: also time these variants of it over all K columns, "
+                    "e.g. np1r12,np1r6,np2r12,np2r6 (np 32-column sub-panels per wave, r B-operand ring slots)")
     args = ap.parse_args()
     import torch
     import spmm_amd as S
@@ -93,11 +95,14 @@ def main():
     if args.lr_lib:
         LR = C.CDLL(str(ROOT / args.lr_lib))
         LR.mfma_probe_launch.argtypes = L.mfma_probe_launch.argtypes
+        LR.mfma_probe_launch_v.argtypes = [C.c_int] + [C.c_void_p] * 6 + [C.c_longlong, C.c_void_p, C.c_int, C.c_int,
+                                                                           C.c_int, C.c_void_p]
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     k = args.k
-    assert k == 32, "probe: one 32-column panel"
+    assert k == 32 or args.no_forced, "probe: one 32-column panel (K > 32 only with --no-forced)"
+    assert k % 32 == 0
 
     def timed(fn):
         ts = []
@@ -160,9 +165,14 @@ def main():
                 d_pos = d(np.concatenate([pos, np.zeros(8, np.uint16)]).view(np.int16))
                 Cm = torch.zeros_like(C_ref)
                 bb = A.ncols * k * 8
-                launch = lambda xcd=args.xcd: L.mfma_probe_launch(nt, d_tiles.data_ptr(), d_chunks.data_ptr(),
-                                                                  d_tcol.data_ptr(), d_val.data_ptr(), d_pos.data_ptr(),
-                                                                  B.data_ptr(), bb, Cm.data_ptr(), k, xcd, sp)
+                def launch(xcd=args.xcd, lib=L, Cout=None):      # the kernel over every 32-column sub-panel
+                    Co = Cm if Cout is None else Cout
+                    r = 0
+                    for k1 in range(0, k, 32):
+                        r |= lib.mfma_probe_launch(nt, d_tiles.data_ptr(), d_chunks.data_ptr(), d_tcol.data_ptr(),
+                                                   d_val.data_ptr(), d_pos.data_ptr(), B.data_ptr() + 8 * k1,
+                                                   bb - 8 * k1, Co.data_ptr() + 8 * k1, k, xcd, sp)
+                    return r
                 st = launch()
                 torch.cuda.synchronize()
                 assert st == 0, st
@@ -180,14 +190,22 @@ def main():
                     case[f"dbg{v}_ms"] = round(timed(lambda: launch(v)), 5)
                 if LR is not None:
                     Cl = torch.zeros_like(C_ref)
-                    lr = lambda xcd=args.xcd: LR.mfma_probe_launch(nt, d_tiles.data_ptr(), d_chunks.data_ptr(),
-                                                                   d_tcol.data_ptr(), d_val.data_ptr(), d_pos.data_ptr(),
-                                                                   B.data_ptr(), bb, Cl.data_ptr(), k, xcd, sp)
+                    lr = lambda: launch(lib=LR, Cout=Cl)
                     assert lr() == 0
                     torch.cuda.synchronize()
                     case["lr_same_as_mfma"] = bool(torch.equal(Cl[rows].view(torch.int64), Cm[rows].view(torch.int64)))
                     case["lr_bitexact"] = bool(torch.equal(Cl[ex].view(torch.int64), C_ref[ex].view(torch.int64)))
                     case["lr_ms"] = round(timed(lr), 5)
+                    for v in (x for x in args.variants.split(",") if x):
+                        npv, rv = int(v[2]), int(v.split("r")[1])
+                        Cl.zero_()
+                        fv = lambda: LR.mfma_probe_launch_v(nt, d_tiles.data_ptr(), d_chunks.data_ptr(),
+                                                            d_tcol.data_ptr(), d_val.data_ptr(), d_pos.data_ptr(),
+                                                            B.data_ptr(), bb, Cl.data_ptr(), k, npv, rv, sp)
+                        assert fv() == 0
+                        torch.cuda.synchronize()
+                        case[f"{v}_same"] = bool(torch.equal(Cl[rows].view(torch.int64), Cm[rows].view(torch.int64)))
+                        case[f"{v}_ms"] = round(timed(fv), 5)
                     del Cl
                 if args.no_forced:
                     tile_nnz = int(np.diff(A.row_ptr)[plan["in_tile"]].sum())
