@@ -12,6 +12,7 @@ cover.
   python tools/summarize_ab.py profiles/r04/ab_changed*.jsonl.gz --census profiles/r04/plan_census.jsonl.gz
 """
 import argparse
+import glob
 import gzip
 import json
 import math
@@ -22,7 +23,7 @@ import numpy as np
 
 def load(paths):
     recs = {}
-    for p in paths:
+    for p in [f for pat in paths for f in sorted(glob.glob(pat))]:
         op = gzip.open if str(p).endswith(".gz") else open
         for line in op(p, "rt"):
             if line.startswith("{"):
