@@ -1031,6 +1031,10 @@ constexpr double MFMA_TILE_NPC = 96.0;      // nonzeros per chunk for a tile to 
 constexpr double MFMA_MIN_TILE_FRAC = 0.9;  // partial coverage lost in the fit sample (tiles beside busy row blocks)
 constexpr double MFMA_MIN_GAIN = 1.30;      // in the fit sample: no taken line below 0.95x, every class >= 1.04x
 constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
+// One 32-column sub-panel (K < 64): rows averaging fewer nonzeros keep the row kernel.  The changed-lines sweep of the
+// round-4 census measured avg-10 and avg-20 lines at K = 32 at 0.79x / 0.95x (median, one worker alone on the GPU),
+// where the model above predicted 1.38 / 1.37; at K = 128 the avg-20 lines gain 1.16x.
+constexpr double MFMA_K32_MIN_ROW_NNZ = 32.0;
 struct MfmaGate {
     int sampled = 0;          // candidate tiles sampled (all rows <= T, not empty)
     double r16 = 0.0;         // mean reuse of the sampled tiles (nonzeros per union column)
@@ -1096,7 +1100,8 @@ void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k, int kw) {
     const double t_left = ROW_US_LAUNCH + P * (((double)nnz - g.tile_nnz) * r_row + left_rows * ROW_US_ROW);
     g.t_on = std::max(t_tiles, t_left);
     g.verdict = (g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.tile_nnz >= MFMA_MIN_TILE_FRAC * (double)nnz &&
-                 g.t_off >= MFMA_MIN_GAIN * g.t_on) ? 1 : 0;
+                 g.t_off >= MFMA_MIN_GAIN * g.t_on && (k >= 64 || (double)nnz >= MFMA_K32_MIN_ROW_NNZ * (double)m))
+                    ? 1 : 0;
 }
 
 // Everything the inspector decides for (matrix, K), on the host: the plan, the tile plan, the block decomposition,
