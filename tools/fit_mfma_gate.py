@@ -84,9 +84,11 @@ def model(F, c):
 
 
 def decide(F, c):
-    """The gate: tiles hold at least MIN_TILE_FRAC of the nonzeros and the model's gain reaches c["gain"]."""
+    """The gate: tiles hold at least MIN_TILE_FRAC of the nonzeros, the model's gain reaches c["gain"], and with one
+    32-column sub-panel (K < 64) rows average at least c["k32_min_row_nnz"] nonzeros."""
     m_on, m_off = model(F, c)
-    return (F["est_tile_nnz"] >= c["min_tile_frac"] * F["nnz"]) & (F["est_tiles"] > 0) & (m_off >= c["gain"] * m_on)
+    return ((F["est_tile_nnz"] >= c["min_tile_frac"] * F["nnz"]) & (F["est_tiles"] > 0) & (m_off >= c["gain"] * m_on) &
+            ((F["k"] >= 64) | (F["nnz"] >= c.get("k32_min_row_nnz", 0.0) * F["m"])))
 
 
 def fit(args):
