@@ -10,6 +10,10 @@ census of the same build, tools/plan_census.py) it also reports how many of the 
 cover.
 
   python tools/summarize_ab.py profiles/r04/ab_changed*.jsonl.gz --census profiles/r04/plan_census.jsonl.gz
+
+With --solo, records of those files (the same A/B timed by ONE process alone on the GPU) replace the records of the
+same (line, K); with --only-changed only the census' changed pairs are tabulated.  The table then says how many of
+each class's timings come from solo runs.
 """
 import argparse
 import glob
@@ -37,8 +41,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("files", nargs="+")
     ap.add_argument("--census", default=None)
+    ap.add_argument("--solo", nargs="*", default=[])
+    ap.add_argument("--only-changed", action="store_true")
     args = ap.parse_args()
     recs = load(args.files)
+    solo = load(args.solo) if args.solo else {}
+    for key, r in solo.items():
+        r["_solo"] = True
+        recs[key] = r
     out = []
     if args.census:
         changed = set()
@@ -49,7 +59,10 @@ def main():
                 changed.add((d["gen"], d["k"]))
         have = {(g, k) for (g, k, _dt) in recs}
         out.append(f"Census: {len(changed)} (line, K) pairs take matrix-core tiles; A/B records cover "
-                   f"{len(changed & have)} of them ({len(have - changed)} records of other pairs).\n")
+                   f"{len(changed & have)} of them ({len(have - changed)} records of other pairs); "
+                   f"{sum(1 for (g, k, _d), r in recs.items() if r.get('_solo') and (g, k) in changed)} timed solo.\n")
+        if args.only_changed:
+            recs = {key: r for key, r in recs.items() if (key[0], key[1]) in changed}
     for K in sorted({k for (_, k, _) in recs}):
         rows = defaultdict(list)
         for (g, k, dt), r in recs.items():
@@ -57,8 +70,8 @@ def main():
                 p = g.split()
                 rows[(int(p[2]), float(p[6]), float(p[9]))].append(r)
         out.append(f"\n### K = {K}\n")
-        out.append("| avg | bw | crs | lines | agg GFLOP/s shipped | agg GFLOP/s no-MFMA | agg ratio | geo-mean | worst | "
-                   "< 0.9x | < 1.0x | median frac | parity |")
+        out.append("| avg | bw | crs | lines (solo) | agg GFLOP/s shipped | agg GFLOP/s no-MFMA | agg ratio | geo-mean | "
+                   "worst | < 0.9x | < 1.0x | median frac | parity |")
         out.append("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
         tot = [0.0, 0.0, 0.0, []]
         for key in sorted(rows):
@@ -74,7 +87,8 @@ def main():
             tot[1] += t_on
             tot[2] += t_off
             tot[3] += list(sp)
-            out.append(f"| {key[0]} | {key[1]} | {key[2]} | {len(rs)} | {fl / t_on / 1e9:,.0f} | {fl / t_off / 1e9:,.0f} | "
+            ns = sum(1 for r in rs if r.get("_solo"))
+            out.append(f"| {key[0]} | {key[1]} | {key[2]} | {len(rs)} ({ns}) | {fl / t_on / 1e9:,.0f} | {fl / t_off / 1e9:,.0f} | "
                        f"{t_off / t_on:.3f} | {math.exp(np.log(sp).mean()):.3f} | {sp.min():.3f} | {(sp < 0.9).sum()} | "
                        f"{(sp < 1.0).sum()} | {np.median(fr):.3f} | {'ok' if par else 'FAIL'} |")
         sp = np.array(tot[3])
