@@ -9,7 +9,8 @@ flags (exact rows of both plans bit-identical; the oracle check of the shipped p
 census of the same build, tools/plan_census.py) it also reports how many of the changed (line, K) pairs the records
 cover.
 
-  python tools/summarize_ab.py profiles/r04/ab_changed*.jsonl.gz --census profiles/r04/plan_census.jsonl.gz
+  python tools/summarize_ab.py profiles/r04/sweep/ab_changed_8w.jsonl.gz --solo profiles/r04/sweep/ab_recheck_solo.jsonl.gz \
+      profiles/r04/sweep/ab_solo.jsonl.gz --census profiles/r04/plan_census.jsonl.gz --only-changed
 
 With --solo, records of those files (the same A/B timed by ONE process alone on the GPU) replace the records of the
 same (line, K); with --only-changed only the census' changed pairs are tabulated.  The table then says how many of
