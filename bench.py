@@ -9,8 +9,10 @@ JSON line.
 
 The line (default, --workload config2):
   value     config 2 (BASELINE.json configs[1]): generator line
-            1000000 1000000 20 6.6667 normal random 0.3 100 0.95 0.5 14, K=32 fp64 -- the same fixed matrix at every
-            N, split N ways (strong scaling), so the driver's 1/2/4/8 values form one curve.  value = 2*nnz*K*steps /
+            1000000 1000000 20 6.6667 normal random 0.3 100 0.95 0.5 14, K=32 fp64; at N > 1 one such matrix per
+            GPU (weak scaling, the default: the path partitions into independent row shards with no collective in the
+            timed step -- every rank owns a config-2-sized nnz-balanced row range of one N-times-larger matrix of the
+            same shape; --scaling strong splits the single config-2 matrix N ways instead).  value = 2*nnz*K*steps /
             (max over ranks of the HIP-event time of the K timed steps on the launch stream); the
             barrier-inclusive wall time is reported beside it ("wall_ms_per_step").
   dataset   (N=1 only; --no-dataset skips it) the metric's own workload, BASELINE "synthetic medium dataset, K=32
@@ -32,9 +34,10 @@ reference harness's column-major layout [K][ncols] (the x the CPU baseline multi
 engine's row-major layout; dataset / twins: torch.rand(seed 42) on the device (copied back column-major for the
 CPU baseline).  Everything resident in HBM in the timed region.
 
-Multi-GPU (--scaling, default strong): STRONG = one fixed global matrix split into N nnz-balanced row ranges with
-the reference partitioner loop_partitioner_balance_prefix_sums (lib/parallel_util.h:141-165).  WEAK = N stacked
-copies of the line's shape (bw/N).  Each rank generates only its rows; B is broadcast from rank 0 once at setup
+Multi-GPU (--scaling, default weak): WEAK = the line's shape N times over (N x rows, N x columns, bw/N: the same
+absolute column window) split into N nnz-balanced row ranges with the reference partitioner
+loop_partitioner_balance_prefix_sums (lib/parallel_util.h:141-165), so every GPU carries one line's work.  STRONG =
+the line's matrix itself split N ways (a fixed global problem).  Each rank generates only its rows; B is broadcast from rank 0 once at setup
 (timed); C stays sharded in the timed loop and is all-gathered once afterwards (timed).  --dist-backend gloo (test
 mode) lets several ranks share one GPU (collectives staged through host memory).
 
@@ -93,7 +96,7 @@ def parse():
     ap.add_argument("--pipe-band", type=int, default=16)
     ap.add_argument("--pipe-mode", type=int, default=0, help="pipeline: SDDMM flags (0 reference, 1 QK^T, |2 softmax)")
     ap.add_argument("--gen", default=None, help="override: 11-field generator line of the global matrix")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: test mode, ranks may share one GPU (collectives staged through host memory)")
     ap.add_argument("--dump-c", default=None, help="rank 0 writes a row sample of the (gathered) C + exact mask (npz)")

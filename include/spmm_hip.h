@@ -75,7 +75,7 @@ int spmm_hip_run(spmm_hip_t *h, const void *x, void *y, int32_t k);
  * internal row-major buffer first, as a separate kernel); d_c: device C row-major [m][k].  stream: a hipStream_t
  * (NULL = the null stream).
  * Concurrency: a handle owns per-run device scratch (the transposed B, split-row partial slots and their arrival
- * counters), so calls on ONE handle must be serialised on ONE stream (as the reference's plugin is not reentrant,
+ * counters, the matrix-core plans' out-of-range flag of B, keyed by the handle's launch count), so calls on ONE handle must be serialised on ONE stream (as the reference's plugin is not reentrant,
  * SURVEY §8b).  Two runs of the same handle in flight on different streams race on that scratch; use one handle
  * per stream instead.  A COL_MAJOR run overwrites the internal B, so it also invalidates the upload cache of
  * spmm_hip_run (SPMM_HIP_ASSUME_X_UNCHANGED). */

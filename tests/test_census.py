@@ -101,3 +101,23 @@ def test_plan_without_tiles_is_config3_plan():
     res = plan_vs_r03.compare(stride=997, max_nnz=3e6, workers=1)
     assert len(res) >= 20
     assert [r for r in res if r[2]] == []
+
+
+def test_gate_only_checks_sampled_columns(S):
+    """Gate-only mode reads the sampled rows' columns only -- and range-checks them (they index host arrays of ncols
+    entries); a bad column outside the sample is never read."""
+    p = S.gen_params(LINES[3])
+    A = S.generate(p)
+    mask = S.gate_sample_rows(A.m).astype(bool)
+    sel = np.repeat(mask, np.diff(A.row_ptr))
+    inside, outside = np.flatnonzero(sel), np.flatnonzero(~sel)
+    assert len(inside) and len(outside)
+    for j, bad in ((inside[len(inside) // 2], True), (outside[len(outside) // 2], False)):
+        for v in (-1, A.ncols):
+            col = A.col_idx.copy()
+            col[j] = v
+            if bad:
+                with pytest.raises(RuntimeError, match="out of range"):
+                    S.debug_plan(A.row_ptr, col, A.ncols, 32, gate_only=True)
+            else:
+                S.debug_plan(A.row_ptr, col, A.ncols, 32, gate_only=True)

@@ -64,8 +64,11 @@ def _worker(rank, world, port, outdir, gen, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,gen,world", [("weak", GEN_WEAK, 2), ("weak", GEN_WEAK, 3),
-                                            ("strong", GEN_STRONG, 2), ("strong", GEN_STRONG, 3)])
+# world 8: the driver's 8-GPU node, rehearsed on CPU ranks (config 4's shape in miniature, and the weak split that
+# bench.py runs by default at N > 1)
+@pytest.mark.parametrize("mode,gen,world", [("weak", GEN_WEAK, 2), ("weak", GEN_WEAK, 3), ("weak", GEN_WEAK, 8),
+                                            ("strong", GEN_STRONG, 2), ("strong", GEN_STRONG, 3),
+                                            ("strong", GEN_STRONG, 8)])
 def test_sharded_equals_whole(tmp_path, mode, gen, world):
     import spmm_amd as S
     from spmm_amd import sharding

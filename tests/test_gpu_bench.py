@@ -33,8 +33,8 @@ def _bench(args, timeout=600):
 
 def test_bench_two_ranks_share_one_gpu(tmp_path):
     c2, c1 = tmp_path / "c2.npz", tmp_path / "c1.npz"
-    two = _bench(["--gpus", "2", "--workload", "config2", "--dist-backend", "gloo", "--steps", "5", "--warmup", "2",
-                  "--no-cpu-baseline", "--dump-c", str(c2)])
+    two = _bench(["--gpus", "2", "--workload", "config2", "--scaling", "strong", "--dist-backend", "gloo",
+                  "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--dump-c", str(c2)])
     assert two["n_gpus"] == 2 and two["config"]["dist_backend"] == "gloo"
     assert sum(two["config"]["nnz_per_rank"]) == two["config"]["nnz_total"]
     assert two["setup"]["selfcheck_all_ranks_ok"] is True
