@@ -312,8 +312,9 @@ void launch_mfma(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
 
 // The matrix-core tiles' exact range (spmm_mfma.hpp): B's check, on the row kernel's stream (beside the tiles when
 // that is the side stream) -- an out-of-range B stores this launch's sequence number into mflag[1] (no reset launch;
-// a stale number of an earlier launch never matches, and under a graph replay a baked-in number can only keep the
-// exact fallback on, never skip it) ...
+// under a graph replay a baked-in number can only keep the exact fallback on, never skip it).  One slot per handle:
+// this relies on the handle's contract that its runs are serialised on one stream (include/spmm_hip.h,
+// spmm_hip_run_device) -- a later launch's flag can then only be stored after this launch's fix-up has read it ...
 template <typename T>
 int launch_mfma_check(spmm_hip_t *h, const T *B, int K, hipStream_t rs) {
     h->mflag_seq = h->mflag_seq == INT32_MAX ? 1 : h->mflag_seq + 1;
@@ -1053,6 +1054,19 @@ inline double mfma_chunks_est(double nnz, double nu) {
     return std::max(std::ceil(nu / MFMA_UC), std::ceil(nnz / room));
 }
 
+// The gate's sample: f(i, r0, r1) for the rows [r0, r1) of sampled candidate tile i (spmm_amd.gate_sample_rows is
+// the same list)
+template <typename F>
+void mfma_gate_tiles(int64_t m, F f) {
+    const int64_t ntiles = (m + MFMA_ROWS - 1) / MFMA_ROWS;
+    const int64_t ns = std::min<int64_t>(MFMA_GATE_SAMPLE, ntiles);
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t t = i * ntiles / ns;
+        const int64_t r0 = t * MFMA_ROWS;
+        f(i, r0, std::min<int64_t>(m, r0 + MFMA_ROWS));
+    }
+}
+
 MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t ncols, int T, double min_reuse,
                      double min_npc) {
     MfmaGate g;
@@ -1061,12 +1075,10 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
     const int64_t ntiles = (m + MFMA_ROWS - 1) / MFMA_ROWS;
     const int64_t ns = std::min<int64_t>(MFMA_GATE_SAMPLE, ntiles);
     double sum_r = 0.0, nz_taken = 0.0, ch_taken = 0.0, n_taken = 0.0;
-    for (int64_t i = 0; i < ns; ++i) {
-        const int64_t t = i * ntiles / ns;
-        const int64_t r0 = t * MFMA_ROWS, r1 = std::min<int64_t>(m, r0 + MFMA_ROWS);
+    mfma_gate_tiles(m, [&](int64_t i, int64_t r0, int64_t r1) {
         bool ok = true;
         for (int64_t r = r0; r < r1 && ok; ++r) ok = (int64_t)rp[r + 1] - rp[r] <= T;
-        if (!ok || rp[r1] == rp[r0]) continue;
+        if (!ok || rp[r1] == rp[r0]) return;
         int64_t nu = 0;
         const double reuse = tile_reuse(rp, col, r0, r1, stamp, (int32_t)i, 0.0, &nu);
         sum_r += reuse;
@@ -1077,7 +1089,7 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
             nz_taken += nnz, ch_taken += ch, n_taken += 1.0;
             g.max_chunks = std::max(g.max_chunks, ch);
         }
-    }
+    });
     if (g.sampled == 0) return g;
     g.r16 = sum_r / g.sampled;
     g.take = n_taken / g.sampled;
@@ -2204,9 +2216,19 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
         if (row_ptr[i + 1] < row_ptr[i]) return fail(SPMM_HIP_ERR_CSR, "debug_plan: row_ptr not monotone");
     const int64_t nnz = row_ptr[m];
     if (nnz > 0 && !col_idx) return fail(SPMM_HIP_ERR_ARG, "debug_plan: col_idx NULL");
-    if (!gate_only)
+    // gate-only mode reads the columns of the gate's sampled rows only (the caller may fill no others): those are
+    // range-checked, as every column is otherwise -- the gate indexes host arrays of ncols entries with them
+    auto col_bad = [&](int64_t j) { return col_idx[j] < 0 || col_idx[j] >= ncols; };
+    if (!gate_only) {
         for (int64_t j = 0; j < nnz; ++j)
-            if (col_idx[j] < 0 || col_idx[j] >= ncols) return fail(SPMM_HIP_ERR_CSR, "debug_plan: col_idx out of range");
+            if (col_bad(j)) return fail(SPMM_HIP_ERR_CSR, "debug_plan: col_idx out of range");
+    } else {
+        bool bad = false;
+        mfma_gate_tiles(m, [&](int64_t, int64_t r0, int64_t r1) {
+            for (int64_t j = row_ptr[r0]; j < row_ptr[r1] && !bad; ++j) bad = col_bad(j);
+        });
+        if (bad) return fail(SPMM_HIP_ERR_CSR, "debug_plan: col_idx out of range (gate sample)");
+    }
     spmm_hip_t h;                 // host-only view: no device state is touched
     h.dtype = dtype;
     h.vsize = dtype == SPMM_HIP_F64 ? 8 : 4;
