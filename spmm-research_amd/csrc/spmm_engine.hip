@@ -290,22 +290,32 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
 // Matrix-core tiles over all K columns (a multiple of 32): four 16-row tiles (one per wave) per workgroup; a wave owns
 // 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (SPMM_HIP_MFMA_NP=1 keeps
 // 32).  The buffer descriptor of B covers the rest of the array from the sub-panel on.
+// B-operand ring (spmm_mfma.hpp): 0 = per sub-panel count default, else SPMM_HIP_MFMA_RING = 6 or 12 slots
+constexpr int MFMA_RING_NP1 = 12, MFMA_RING_NP2 = 12;
 template <typename T>
 void launch_mfma(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
     const int np_max = env_int("SPMM_HIP_MFMA_NP", 2) >= 2 ? 2 : 1;
+    const int ring_env = env_int("SPMM_HIP_MFMA_RING", 0);
     for (int k1 = 0; k1 + 32 <= K;) {
         const int np = (np_max >= 2 && k1 + 64 <= K) ? 2 : 1;
+        const int ring = ring_env == 6 || ring_env == 12 ? ring_env : np == 2 ? MFMA_RING_NP2 : MFMA_RING_NP1;
         const uint32_t bb = (uint32_t)(((size_t)h->ncols * (size_t)K - (size_t)k1) * sizeof(T));
-        auto go = [&](auto xcd_c, auto np_c) {
-            spmm_mfma_tile_kernel<T, decltype(xcd_c)::value, decltype(np_c)::value><<<grid, WG, 0, s>>>(
-                h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const T *)h->d_tval, h->d_tlidx, B + k1, bb,
-                C + k1, K);
+        auto go = [&](auto xcd_c, auto np_c, auto r_c) {
+            spmm_mfma_tile_kernel<T, decltype(xcd_c)::value, decltype(np_c)::value, decltype(r_c)::value>
+                <<<grid, WG, 0, s>>>(h->d_tiles, h->plan.ntile, h->d_tchunk, h->d_tcol, (const T *)h->d_tval,
+                                     h->d_tlidx, B + k1, bb, C + k1, K);
         };
         using N1 = std::integral_constant<int, 1>;
         using N2 = std::integral_constant<int, 2>;
-        if (h->plan.tile_xcd) np == 2 ? go(std::true_type(), N2()) : go(std::true_type(), N1());
-        else np == 2 ? go(std::false_type(), N2()) : go(std::false_type(), N1());
+        using R6 = std::integral_constant<int, 6>;
+        using R12 = std::integral_constant<int, MFMA_KS>;
+        auto go_r = [&](auto xcd_c) {
+            if (np == 2) ring == 6 ? go(xcd_c, N2(), R6()) : go(xcd_c, N2(), R12());
+            else ring == 6 ? go(xcd_c, N1(), R6()) : go(xcd_c, N1(), R12());
+        };
+        if (h->plan.tile_xcd) go_r(std::true_type());
+        else go_r(std::false_type());
         k1 += 32 * np;
     }
 }
@@ -1019,23 +1029,29 @@ constexpr int MFMA_GATE_SAMPLE = 256;
 // afterwards (nochk / checked = 0.88-0.89, profiles/r04/s_b/kt.log).  A tile is taken when it brings at least
 // MFMA_TILE_NPC nonzeros per chunk; a matrix takes matrix-core tiles when they hold MFMA_MIN_TILE_FRAC of its
 // nonzeros and the model's time with them (tiles beside the leftover rows) beats the row kernel's by MFMA_MIN_GAIN.
-constexpr double MFMA_US_CHUNK = 1.385e-3;
-constexpr double MFMA_US_TILE = 1.36e-3;
-constexpr double MFMA_US_CHAIN = 1.01;
-constexpr double MFMA_US_LAUNCH = 22.0;
-constexpr double ROW_US_LAUNCH = 7.2;
-constexpr double ROW_US_NNZ = 1.877e-5;     // x reuse^-ROW_REUSE_EXP x (kw / 32)^-ROW_KW_EXP
-constexpr double ROW_REUSE_EXP = 0.148;
-constexpr double ROW_KW_EXP = 0.200;
-constexpr double ROW_US_ROW = 7.05e-5;
-constexpr double MFMA_TILE_NPC = 96.0;      // nonzeros per chunk for a tile to be taken
-constexpr double MFMA_MIN_TILE_FRAC = 0.9;  // partial coverage lost in the fit sample (tiles beside busy row blocks)
-constexpr double MFMA_MIN_GAIN = 1.30;      // in the fit sample: no taken line below 0.95x, every class >= 1.04x
+// One constant set per value type (the matrix-core tile kernel, its B operand and the row kernel's gather all differ
+// in width between fp64 and fp32).  `on` = false: the default policy never takes matrix-core tiles for that type
+// (SPMM_HIP_MFMA >= 1 still does).
+struct GateModel {
+    double us_chunk, us_tile, us_chain, us_launch;     // tile kernel
+    double row_launch, row_nnz, row_reuse_exp, row_kw_exp, row_row;   // row kernel
+    double npc;              // nonzeros per chunk for a tile to be taken (MFMA_TILE_NPC)
+    double min_tile_frac;    // taken tiles must hold this share of the nonzeros
+    double min_gain;         // model gain the gate asks for
+    double k32_min_row_nnz;  // one 32-column sub-panel (K < 64): rows must average this many nonzeros
+    bool on;
+};
+// fp64: round-4 fit (598 pairs, profiles/r04/s_c/), tile constants x 0.9 (the range check left the MFMA loop);
+// K < 64 rule: the changed-lines sweep of the round-4 census measured avg-10 / avg-20 lines at K = 32 at 0.79x /
+// 0.95x (median, one worker alone on the GPU) where the model predicted 1.38 / 1.37.
+constexpr GateModel GATE_F64 = {1.385e-3, 1.36e-3, 1.01, 22.0, 7.2, 1.877e-5, 0.148, 0.200, 7.05e-5,
+                                96.0, 0.9, 1.30, 32.0, true};
+// fp32: not fitted yet -- the fp64 constants, and off under the default policy (three fp32 twins ran
+// 0.88-0.94x with fp64-fitted tiles)
+constexpr GateModel GATE_F32 = {1.385e-3, 1.36e-3, 1.01, 22.0, 7.2, 1.877e-5, 0.148, 0.200, 7.05e-5,
+                                96.0, 0.9, 1.30, 32.0, false};
+inline const GateModel &gate_model(size_t vsize) { return vsize == 8 ? GATE_F64 : GATE_F32; }
 constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
-// One 32-column sub-panel (K < 64): rows averaging fewer nonzeros keep the row kernel.  The changed-lines sweep of the
-// round-4 census measured avg-10 and avg-20 lines at K = 32 at 0.79x / 0.95x (median, one worker alone on the GPU),
-// where the model above predicted 1.38 / 1.37; at K = 128 the avg-20 lines gain 1.16x.
-constexpr double MFMA_K32_MIN_ROW_NNZ = 32.0;
 struct MfmaGate {
     int sampled = 0;          // candidate tiles sampled (all rows <= T, not empty)
     double r16 = 0.0;         // mean reuse of the sampled tiles (nonzeros per union column)
@@ -1101,18 +1117,18 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
 }
 
 // The gate: the cost model above for the K columns in 32-column sub-panels.
-void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k, int kw) {
+void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k, int kw, const GateModel &c) {
     const double P = (double)k / 32.0;
-    const double r_row = ROW_US_NNZ * std::pow(std::max(g.r16, 1.0), -ROW_REUSE_EXP) *
-                         std::pow((double)std::max(kw, 1) / 32.0, -ROW_KW_EXP);
-    g.t_off = ROW_US_LAUNCH + P * ((double)nnz * r_row + (double)m * ROW_US_ROW);
-    const double t_tiles = MFMA_US_LAUNCH + P * std::max(g.chunks * MFMA_US_CHUNK + g.tiles * MFMA_US_TILE,
-                                                         g.max_chunks * MFMA_US_CHAIN);
+    const double r_row = c.row_nnz * std::pow(std::max(g.r16, 1.0), -c.row_reuse_exp) *
+                         std::pow((double)std::max(kw, 1) / 32.0, -c.row_kw_exp);
+    g.t_off = c.row_launch + P * ((double)nnz * r_row + (double)m * c.row_row);
+    const double t_tiles = c.us_launch + P * std::max(g.chunks * c.us_chunk + g.tiles * c.us_tile,
+                                                      g.max_chunks * c.us_chain);
     const double left_rows = std::max((double)m - (double)MFMA_ROWS * g.tiles, 0.0);
-    const double t_left = ROW_US_LAUNCH + P * (((double)nnz - g.tile_nnz) * r_row + left_rows * ROW_US_ROW);
+    const double t_left = c.row_launch + P * (((double)nnz - g.tile_nnz) * r_row + left_rows * c.row_row);
     g.t_on = std::max(t_tiles, t_left);
-    g.verdict = (g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.tile_nnz >= MFMA_MIN_TILE_FRAC * (double)nnz &&
-                 g.t_off >= MFMA_MIN_GAIN * g.t_on && (k >= 64 || (double)nnz >= MFMA_K32_MIN_ROW_NNZ * (double)m))
+    g.verdict = (c.on && g.tiles > 0 && nnz >= MFMA_GATE_MIN_NNZ && g.tile_nnz >= c.min_tile_frac * (double)nnz &&
+                 g.t_off >= c.min_gain * g.t_on && (k >= 64 || (double)nnz >= c.k32_min_row_nnz * (double)m))
                     ? 1 : 0;
 }
 
@@ -1248,9 +1264,10 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
                 const bool force_all = forced > 0 || fm == 1;
                 const double treuse = (mthr && *mthr) ? atof(mthr) : force_all ? 1.0 : MFMA_TILE_REUSE;
                 const char *npc_env = getenv("SPMM_HIP_MFMA_NPC");   // measurement override of MFMA_TILE_NPC
-                const double npc = force_all ? 0.0 : (npc_env && *npc_env) ? atof(npc_env) : MFMA_TILE_NPC;
+                const GateModel &gm = gate_model(h->vsize);
+                const double npc = force_all ? 0.0 : (npc_env && *npc_env) ? atof(npc_env) : gm.npc;
                 d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, treuse, npc);
-                mfma_cost(d.gate, h->m, h->nnz, k, pl.kw);
+                mfma_cost(d.gate, h->m, h->nnz, k, pl.kw, gm);
                 pl.tile_reuse = d.gate.r16;
                 if (gate_only) {
                     d.gate_only = true;
@@ -2272,8 +2289,10 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     return SPMM_HIP_OK;
 }
 
-int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, const double *sample, double *out) {
-    if (!sample || !out || m < 0 || nnz < 0 || k < 1 || kw < 1) return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
+int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, int32_t dtype, const double *sample,
+                        double *out) {
+    if (!sample || !out || m < 0 || nnz < 0 || k < 1 || kw < 1 || (dtype != SPMM_HIP_F64 && dtype != SPMM_HIP_F32))
+        return fail(SPMM_HIP_ERR_ARG, "debug_gate: bad arguments");
     MfmaGate g;
     g.sampled = (int)sample[0];
     g.r16 = sample[1];
@@ -2282,7 +2301,7 @@ int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, const dou
     g.tile_nnz = sample[4];
     g.chunks = sample[5];
     g.max_chunks = sample[6];
-    mfma_cost(g, m, nnz, k, kw);
+    mfma_cost(g, m, nnz, k, kw, gate_model(dtype == SPMM_HIP_F64 ? 8 : 4));
     out[0] = g.verdict;
     out[1] = g.t_on;
     out[2] = g.t_off;

@@ -96,12 +96,20 @@ template <> struct MfmaT<float> {
     __device__ static float fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 };
 
+// Waves per SIMD the register budget allows: a whole chunk of B operands in flight (R = 12) costs 4 VGPRs per slot and
+// sub-panel; a ring of R < 12 slots (the operand of step s + R loaded once step s's MFMAs have issued) frees them.
+template <typename T, int NP, int R>
+constexpr int mfma_waves() {
+    return sizeof(T) == 4 ? (R < MFMA_KS ? 4 : 3) : (NP == 1 ? (R < MFMA_KS ? 4 : 3) : (R < MFMA_KS ? 3 : 2));
+}
+
 // No range check here: mfma_fixup_kernel recomputes every tile when an operand lies outside the exact range
-template <typename T, bool XCD, int NP>
-__global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm_mfma_tile_kernel(
+template <typename T, bool XCD, int NP, int R = MFMA_KS>
+__global__ __launch_bounds__(256, (mfma_waves<T, NP, R>())) void spmm_mfma_tile_kernel(
     const int4 *__restrict__ tiles, int ntiles, const int4 *__restrict__ tchunk, const int32_t *__restrict__ tcolT,
     const T *__restrict__ tval, const uint16_t *__restrict__ tpos, const T *__restrict__ B, uint32_t b_bytes,
     T *__restrict__ C, int ld) {
+    static_assert(R >= 1 && R <= MFMA_KS && MFMA_KS % R == 0, "ring slots");
     using M = MfmaT<T>;
     typedef typename M::acc_t acc_t;
     typedef typename M::bop_t bop_t;
@@ -122,22 +130,42 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
     acc_t acc[NP][2];
 #pragma unroll
     for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = acc_t{T(0), T(0), T(0), T(0)};
-    bop_t bo[NP][MFMA_KS];
-    int tcn[MFMA_KS];
+    bop_t bo[NP][R];
+    int tcn[MFMA_KS];       // R = 12: union columns of the chunk whose B operand is being loaded (c+1 in iteration c)
+    int tn = 0;             // lane < 48: one union column of chunk c+2, fetched an iteration ahead
     T ev[MFMA_NPE];
     int ep[MFMA_NPE], hc[MFMA_NPE];
     int ne = 0;
-    auto load_tcol = [&](int c) {                 // this lane's 12 union columns of chunk c (3 x 16 B)
-        const i32x4 *p = reinterpret_cast<const i32x4 *>(tcolT + (size_t)(tl.z + c) * MFMA_UC + g * MFMA_KS);
+    // Vector-memory results are waited for in issue order (s_waitcnt vmcnt): a wait for one load drags every older load
+    // with it, and the compiler's waits are static, sized for every path into a block.  So a register the loop's B
+    // loads address with must never be a vector-memory destination on any path: the union columns go global -> VGPR
+    // (tn, fetched at the TOP of iteration c for chunk c+2, ahead of the B loads issued during its MFMAs) -> LDS (end
+    // of the iteration: waits only for loads a whole iteration old) -> the B loads' addresses (LDS reads).  The
+    // prologue issues its loads in the loop's order, so the first iteration's waits are the steady state's.
+    // (Round 4's kernel fetched the columns after the B loads: the next chunk's first B load waited for all of them,
+    // one exposed memory latency per chunk.)
+    __shared__ __attribute__((aligned(16))) int stc[4 * 2 * MFMA_UC];   // per wave: columns of two chunks
+    int *TC = stc + wave * 2 * MFMA_UC;
+    auto fetch_tcol = [&](int c) {
+        if (l < MFMA_UC) tn = __builtin_nontemporal_load(tcolT + (size_t)(tl.z + c) * MFMA_UC + l);
+    };
+    auto put_tcol = [&](int c) {
+        if (l < MFMA_UC) TC[(c & 1) * MFMA_UC + l] = tn;
+    };
+    auto take_tcol = [&](int c) {                 // this lane's 12 columns of chunk c (its k-step group g)
+        const i32x4 *p = reinterpret_cast<const i32x4 *>(TC + (c & 1) * MFMA_UC + g * MFMA_KS);
 #pragma unroll
         for (int q = 0; q < MFMA_KS / 4; ++q) {
             const i32x4 v = p[q];
             tcn[4 * q] = v.x, tcn[4 * q + 1] = v.y, tcn[4 * q + 2] = v.z, tcn[4 * q + 3] = v.w;
         }
     };
-    auto load_b1 = [&](int st) {
+    // B operand of (chunk c, step st) into ring slot st % R; R = 12 addresses with tcn (chunk c's columns, taken at
+    // the top of the iteration), a ring reads each column from LDS when it loads
+    auto load_b = [&](int c, int st) {
+        const int col = R == MFMA_KS ? tcn[st] : TC[(c & 1) * MFMA_UC + g * MFMA_KS + st];
 #pragma unroll
-        for (int p = 0; p < NP; ++p) bo[p][st] = M::load(rs, (uint32_t)tcn[st] * ldb + lane_off + SUB * p);
+        for (int p = 0; p < NP; ++p) bo[p][st % R] = M::load(rs, (uint32_t)col * ldb + lane_off + SUB * p);
     };
     auto load_e = [&](int c) {
         const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
@@ -157,38 +185,46 @@ __global__ __launch_bounds__(256, (NP == 1 || sizeof(T) == 4) ? 3 : 2) void spmm
             hc[j] = cell;
         }
     };
-    // prologue: chunk 0 in the panel, B operand of chunk 0, entries and union columns of chunk 1
-    load_tcol(0);
-#pragma unroll
-    for (int st = 0; st < MFMA_KS; ++st) load_b1(st);
+    // prologue: chunk 0 in the panel; then, in the loop's order, chunk 1's columns, chunk 1's entries, the first R
+    // steps' B operand of chunk 0, chunk 1's columns into LDS
+    fetch_tcol(0);
+    put_tcol(0);
     load_e(0);
     scatter();
+    fetch_tcol(min(1, tl.w - 1));
     load_e(min(1, tl.w - 1));
-    load_tcol(min(1, tl.w - 1));
+    if (R == MFMA_KS) take_tcol(0);
+#pragma unroll
+    for (int st = 0; st < R; ++st) load_b(0, st);
+    put_tcol(1);
     for (int c = 0; c < tl.w; ++c) {
         const int ns = (tchunk[tl.z + c].y + 3) >> 2;
+        fetch_tcol(min(c + 2, tl.w - 1));
+        if (R == MFMA_KS) take_tcol(c + 1);        // chunk c+1's columns (its B operand loads during these MFMAs)
         T a[MFMA_KS];
         const T *pa = P + (l & 15) * MFMA_PST + g;
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
 #pragma unroll
         for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
-        if (c + 1 < tl.w) scatter();
-        load_e(min(c + 2, tl.w - 1));
+        if (c + 1 < tl.w) scatter();             // chunk c+1's entries (ev / ep, loaded an iteration ago) ...
+        load_e(min(c + 2, tl.w - 1));             // ... before the registers take chunk c+2's
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) {
             if (st < ns) {
 #pragma unroll
                 for (int p = 0; p < NP; ++p) {
                     T bb[2];
-                    __builtin_memcpy(bb, &bo[p][st], 2 * sizeof(T));
+                    __builtin_memcpy(bb, &bo[p][st % R], 2 * sizeof(T));
                     acc[p][0] = M::mfma(a[st], bb[0], acc[p][0]);
                     acc[p][1] = M::mfma(a[st], bb[1], acc[p][1]);
                 }
             }
-            load_b1(st);                           // chunk c+1's operand (tcn holds its columns)
+            // the slot just read takes step st + R: of this chunk, or of the next
+            if (st + R < MFMA_KS) load_b(c, st + R);
+            else load_b(c + 1, st + R - MFMA_KS);
         }
-        load_tcol(min(c + 2, tl.w - 1));
+        put_tcol(c + 2);                           // buffer (c & 1): chunk c's columns are no longer read
     }
     const int c0 = 2 * (l & 15);
 #pragma unroll

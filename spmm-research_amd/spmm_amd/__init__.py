@@ -142,7 +142,7 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_debug_tiles_free.argtypes = [C.POINTER(_Tiles)]
     L.spmm_hip_debug_tiles_free.restype = None
     L.spmm_hip_debug_plan.argtypes = [_i32p, _i32p, i64, i64, i32, i32, i32, i32, _f64p]
-    L.spmm_hip_debug_gate.argtypes = [i64, i64, i32, i32, _f64p, _f64p]
+    L.spmm_hip_debug_gate.argtypes = [i64, i64, i32, i32, i32, _f64p, _f64p]
     L.spmm_hip_strerror.argtypes = [C.c_int]
     L.spmm_hip_strerror.restype = C.c_char_p
     L.spmm_hip_last_error_detail.restype = C.c_char_p
@@ -388,11 +388,11 @@ PLAN_FIELDS = ("mode", "gate", "r16", "take", "est_tile_nnz", "est_chunks", "max
 GATE_SAMPLE = ("sampled", "r16", "take", "est_tiles", "est_tile_nnz", "est_chunks", "max_chunks")
 
 
-def debug_gate(m: int, nnz: int, k: int, sample: dict) -> dict:
+def debug_gate(m: int, nnz: int, k: int, sample: dict, dtype: int = F64) -> dict:
     """The matrix-core gate's cost model (spmm_hip_debug_gate) on a recorded gate sample (debug_plan's fields)."""
     v = np.array([float(sample[f]) for f in GATE_SAMPLE], np.float64)
     out = np.zeros(3, np.float64)
-    _check("debug_gate", hip.spmm_hip_debug_gate(int(m), int(nnz), int(k), int(sample["kw"]), v, out))
+    _check("debug_gate", hip.spmm_hip_debug_gate(int(m), int(nnz), int(k), int(sample["kw"]), int(dtype), v, out))
     return {"gate": int(out[0]), "t_on_us": float(out[1]), "t_off_us": float(out[2])}
 
 

@@ -83,3 +83,13 @@ def test_multi_gpu_factory_fails_loudly_without_gpu():
     bad = np.array([0, 2, 1], np.int32)
     assert S.hip.spmm_hip_create_multi(bad, ci, va.ctypes.data_as(ctypes.c_void_p), 2, 2, 1, 4, 0, 2, None,
                                        ctypes.byref(h)) == -6        # malformed CSR (before any device work)
+
+
+@pytest.mark.parametrize("lib", ["libspmm_hip.so", "libspmm_pbv.so"])
+def test_device_code_holds_every_registered_kernel(lib):
+    """Every kernel the host half registers is in the library's gfx950 code objects (tools/check_fatbin.py): a device
+    half compiled from an older source than its host half would load and abort at the first launch."""
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "check_fatbin.py"), str(LIB / lib)], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "missing 0" in r.stdout

@@ -82,10 +82,11 @@ def test_debug_plan_rejects_bad_input(S):
 def test_debug_gate_reproduces_plan_verdict(S, line):
     """spmm_hip_debug_gate on the sample debug_plan reports gives debug_plan's own verdict and model times."""
     A = S.generate(S.gen_params(line))
-    for k in (32, 64, 128):
-        d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, gate_only=True)
-        g = S.debug_gate(A.m, A.nnz, k, d)
-        assert g["gate"] == d["gate"] and g["t_on_us"] == d["t_on_us"] and g["t_off_us"] == d["t_off_us"]
+    for dt in (S.F64, S.F32):
+        for k in (32, 64, 128):
+            d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, dtype=dt, gate_only=True)
+            g = S.debug_gate(A.m, A.nnz, k, d, dtype=dt)
+            assert g["gate"] == d["gate"] and g["t_on_us"] == d["t_on_us"] and g["t_off_us"] == d["t_off_us"]
 
 
 def test_plan_without_tiles_is_config3_plan():

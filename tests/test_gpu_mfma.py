@@ -31,7 +31,7 @@ def bits(a):
 
 
 def handle(S, A, vals, k, monkeypatch, env):
-    for kk in ("SPMM_HIP_TILES", "SPMM_HIP_MFMA", "SPMM_HIP_MFMA_REUSE"):
+    for kk in ("SPMM_HIP_TILES", "SPMM_HIP_MFMA", "SPMM_HIP_MFMA_REUSE", "SPMM_HIP_MFMA_RING"):
         monkeypatch.delenv(kk, raising=False)
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
@@ -55,11 +55,12 @@ MATS = ["6000 6000 100 33 normal random 0.05 0 0.95 0.95 14",          # similar
 
 @pytest.mark.parametrize("line", MATS, ids=["similar", "dense", "split", "lowreuse"])
 @pytest.mark.parametrize("k", [32, 64, 96, 128])
-def test_mfma_bitexact(env, monkeypatch, line, k):
+@pytest.mark.parametrize("ring", ["12", "6"])     # B-operand slots per sub-panel: a whole chunk, or a 6-slot ring
+def test_mfma_bitexact(env, monkeypatch, line, k, ring):
     torch, S, O = env
     A = S.generate(S.gen_params(line))
     x = O.drand48(7 + k, A.ncols * k) * 2.0 - 1.0          # mixed signs: rounding in every chain
-    y1, t1, ex1 = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    y1, t1, ex1 = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1", "SPMM_HIP_MFMA_RING": ring})
     assert t1["mode"] == "mfma" and t1["tiles"] > 0
     y0, t0, ex0 = run(S, A, A.values, x, k, monkeypatch, {"SPMM_HIP_TILES": "-1"})
     assert t0["tiles"] == 0
@@ -369,7 +370,7 @@ def test_multi_handle_tile_mode(env, monkeypatch):
 def test_debug_plan_matches_handle(env, monkeypatch):
     """spmm_hip_debug_plan (host only) reports what the handle planned."""
     torch, S, O = env
-    for kk in ("SPMM_HIP_TILES", "SPMM_HIP_MFMA", "SPMM_HIP_MFMA_REUSE"):
+    for kk in ("SPMM_HIP_TILES", "SPMM_HIP_MFMA", "SPMM_HIP_MFMA_REUSE", "SPMM_HIP_MFMA_RING"):
         monkeypatch.delenv(kk, raising=False)
     for line in ("22354 22354 500 166.6667 normal random 0.05 0 1.4 0.95 14", MATS[2]):
         A = S.generate(S.gen_params(line))
@@ -389,12 +390,13 @@ def test_debug_plan_matches_handle(env, monkeypatch):
 
 @pytest.mark.parametrize("line", MATS, ids=["similar", "dense", "split", "lowreuse"])
 @pytest.mark.parametrize("k", [32, 64, 128])
-def test_mfma_f32_bitexact(env, monkeypatch, line, k):
+@pytest.mark.parametrize("ring", ["12", "6"])
+def test_mfma_f32_bitexact(env, monkeypatch, line, k, ring):
     torch, S, O = env
     A = S.generate(S.gen_params(line))
     vals = (A.values * np.where(np.arange(A.nnz) % 3 == 0, -1.0, 1.0)).astype(np.float32)
     x = (O.drand48(17 + k, A.ncols * k) * 2.0 - 1.0).astype(np.float32)
-    y1, t1, ex1 = run(S, A, vals, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1"})
+    y1, t1, ex1 = run(S, A, vals, x, k, monkeypatch, {"SPMM_HIP_MFMA": "1", "SPMM_HIP_MFMA_RING": ring})
     assert t1["mode"] == "mfma" and t1["tiles"] > 0
     assert ex1.sum() >= t1["rows"] * 0.99                # tile rows are exact rows
     y0, t0, ex0 = run(S, A, vals, x, k, monkeypatch, {"SPMM_HIP_TILES": "-1"})

@@ -26,28 +26,28 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 
 
-def load_ab(patterns):
+def load_ab(patterns, dtype="f64"):
     recs = {}
     for pat in patterns:
         for f in glob.glob(pat):
             for l in open(f):
                 if l.startswith("{"):
                     d = json.loads(l)
-                    if "ms_base" in d:
+                    if "ms_base" in d and d.get("dtype", "f64") == dtype:
                         recs[(d["gen"], d["k"])] = d
     return recs
 
 
 def feat_job(job):
-    line, ks, npc = job
+    line, ks, npc, dtype = job
     os.environ["SPMM_HIP_MFMA_NPC"] = str(npc)
     import spmm_amd as S
     p = S.gen_params(line)
     A = S.generate_masked(p, S.gate_sample_rows(int(p.nr_rows)))
     out = []
     for k in ks:
-        d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, S.F64, 2, gate_only=True)
-        out.append({"gen": line, "k": k, "m": int(A.m), "nnz": int(A.nnz), "npc": npc,
+        d = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, S.F64 if dtype == "f64" else S.F32, 2, gate_only=True)
+        out.append({"gen": line, "k": k, "dtype": dtype, "m": int(A.m), "nnz": int(A.nnz), "npc": npc,
                     **{f: d[f] for f in ("sampled", "r16", "take", "est_tiles", "est_tile_nnz", "est_chunks",
                                          "max_chunks", "seq_max", "kw")}})
     return out
@@ -60,12 +60,12 @@ def features(args):
             if g.strip():
                 lines[g.strip()] = [int(x) for x in args.k.split(",")]
     else:
-        for (g, k) in load_ab(args.ab):
+        for (g, k) in load_ab(args.ab, args.dtype):
             lines[g].append(k)
     os.environ["OMP_NUM_THREADS"] = str(args.threads)
     from multiprocessing import get_context
     with get_context("fork").Pool(args.workers) as pool, open(args.out, "w") as f:
-        for recs in pool.imap_unordered(feat_job, [(g, sorted(ks), args.npc) for g, ks in lines.items()]):
+        for recs in pool.imap_unordered(feat_job, [(g, sorted(ks), args.npc, args.dtype) for g, ks in lines.items()]):
             for r in recs:
                 f.write(json.dumps(r) + "\n")
     print(f"{args.out}: {sum(len(v) for v in lines.values())} (line, K)")
@@ -93,11 +93,12 @@ def decide(F, c):
 
 def fit(args):
     from scipy.optimize import least_squares
-    ab = load_ab(args.ab)
+    ab = load_ab(args.ab, args.dtype)
     feats = {}
     for l in open(args.features):
         d = json.loads(l)
-        feats[(d["gen"], d["k"])] = d
+        if d.get("dtype", "f64") == args.dtype:
+            feats[(d["gen"], d["k"])] = d
     keys = [k for k in ab if k in feats and ab[k]["tile_mode"] == "mfma"]
     F = {f: np.array([feats[k][f] if f in feats[k] else ab[k][f] for k in keys], float)
          for f in ("k", "nnz", "m", "est_chunks", "est_tiles", "est_tile_nnz", "max_chunks", "r16", "kw")}
@@ -147,6 +148,7 @@ def main():
     ap.add_argument("--npc", type=float, default=96.0)
     ap.add_argument("--lines", default=None, help="features: a file of generator lines instead of --ab")
     ap.add_argument("--k", default="32,128")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64", help="the A/B records' and the gate's value type")
     ap.add_argument("--workers", type=int, default=3)
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--out", default=str(ROOT / "profiles" / "r04" / "fit_features.jsonl"))
