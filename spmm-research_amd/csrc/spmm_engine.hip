@@ -201,7 +201,7 @@ bool try_variant(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStrea
 template <typename T, int VEC, int G>
 bool launch_tuned(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
     return TV(16, true, true, false) TV(16, true, false, false) TV(16, true, true, true) TV(16, true, false, true)
-        false;
+        TV(-8, true, false, true) TV(-16, true, false, true) false;
 }
 #endif
 
@@ -291,7 +291,7 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
 // 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (SPMM_HIP_MFMA_NP=1 keeps
 // 32).  The buffer descriptor of B covers the rest of the array from the sub-panel on.
 // B-operand ring (spmm_mfma.hpp): 0 = per sub-panel count default, else SPMM_HIP_MFMA_RING = 6 or 12 slots
-constexpr int MFMA_RING_NP1 = 12, MFMA_RING_NP2 = 12;
+constexpr int MFMA_RING_NP1 = 12, MFMA_RING_NP2 = 6;   // r05b: 6 slots at 64 columns 0.87-1.02x (geomean 0.95)
 template <typename T>
 void launch_mfma(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;

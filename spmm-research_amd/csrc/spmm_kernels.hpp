@@ -85,10 +85,41 @@ struct BGather {
     }
 };
 
+// Software-pipelined row (tuning build: U < 0 selects it with |U| per batch): batch j+1's gathers are issued before
+// batch j's FMAs, so between |U| and 2|U| gathers stay in flight instead of U then none; same FMA order.
+template <typename T, int VEC, int U, typename Gather>
+__device__ __forceinline__ vec<T, VEC> row_dot_pipe(vec<T, VEC> acc, const int32_t *s_col, const T *s_val, int a,
+                                                    int e, const Gather &gather) {
+    using V = vec<T, VEC>;
+    V b0[U], b1[U];
+    auto issue = [&](V *b, int j) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u < e) b[u] = gather(s_col[j + u]);
+    };
+    auto fold = [&](const V *b, int j) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u < e) vfma(acc, s_val[j + u], b[u]);
+    };
+    int j = a;
+    if (j < e) issue(b0, j);
+    while (j < e) {
+        issue(b1, j + U);
+        fold(b0, j);
+        j += U;
+        if (j >= e) break;
+        issue(b0, j + U);
+        fold(b1, j);
+        j += U;
+    }
+    return acc;
+}
+
 // One virtual row, nonzeros [a, e) of the LDS-staged block: U gathers in flight, then U FMAs in CSR order.
 template <typename T, int VEC, int U, typename Gather>
-__device__ __forceinline__ vec<T, VEC> row_dot(vec<T, VEC> acc, const int32_t *s_col, const T *s_val, int a, int e,
-                                               const Gather &gather) {
+__device__ __forceinline__ vec<T, VEC> row_dot_batch(vec<T, VEC> acc, const int32_t *s_col, const T *s_val, int a,
+                                                     int e, const Gather &gather) {
     using V = vec<T, VEC>;
     int j = a;
     for (; j + U <= e; j += U) {
@@ -108,6 +139,13 @@ __device__ __forceinline__ vec<T, VEC> row_dot(vec<T, VEC> acc, const int32_t *s
             if (j + u < e) vfma(acc, s_val[j + u], bv[u]);
     }
     return acc;
+}
+
+template <typename T, int VEC, int U, typename Gather>
+__device__ __forceinline__ vec<T, VEC> row_dot(vec<T, VEC> acc, const int32_t *s_col, const T *s_val, int a, int e,
+                                               const Gather &gather) {
+    if constexpr (U < 0) return row_dot_pipe<T, VEC, -U>(acc, s_col, s_val, a, e, gather);
+    else return row_dot_batch<T, VEC, U>(acc, s_col, s_val, a, e, gather);
 }
 
 // Strided piece of a virtual row for vector lanes: nonzeros a, a+L, a+2L, ... < e (L = 1: the whole row, in order).
@@ -371,7 +409,8 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
                 dst = C + (size_t)(r0 + r) * ld;
             }
             if (VL && L > 1) {   // block-uniform branch: L = 1 blocks run the plain unit-stride chain below
-                acc = row_dot_strided<T, VEC, U / 2>(acc, s_col, s_val, s_rp[r] - jb + sub, s_rp[r + 1] - jb, L, gather);
+                acc = row_dot_strided<T, VEC, (U < 0 ? -U : U) / 2>(acc, s_col, s_val, s_rp[r] - jb + sub, s_rp[r + 1] - jb,
+                                                                    L, gather);
                 for (int off = (G * L) >> 1; off >= G; off >>= 1) vshfl_add(acc, off);   // fixed tree over sub-lanes
                 if (sub == 0) {
                     if (MODE == DEST_SPLIT && sc1) vstore_sc1<T, VEC>(prs, poff, acc);
