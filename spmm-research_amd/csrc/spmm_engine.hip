@@ -291,7 +291,7 @@ void launch_tiles(spmm_hip_t *h, const T *B, T *C, int ld, int kw, hipStream_t s
 // 64 columns (two 32-column sub-panels, NP = 2) where two are left, else 32 (SPMM_HIP_MFMA_NP=1 keeps
 // 32).  The buffer descriptor of B covers the rest of the array from the sub-panel on.
 // B-operand ring (spmm_mfma.hpp): 0 = per sub-panel count default, else SPMM_HIP_MFMA_RING = 6 or 12 slots
-constexpr int MFMA_RING_NP1 = 12, MFMA_RING_NP2 = 6;   // r05b: 6 slots at 64 columns 0.87-1.02x (geomean 0.95)
+constexpr int MFMA_RING_NP1 = 6, MFMA_RING_NP2 = 6;   // r05b: 6 slots 0.94-1.03x at 32 columns, 0.87-1.02x at 64
 template <typename T>
 void launch_mfma(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s) {
     const int grid = (h->plan.ntile + 3) / 4;
@@ -1739,8 +1739,22 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tchunk, tp.chunks.data(), tp.chunks.size() * sizeof(int4));
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tcol, tcolT.data(), tcolT.size() * 4);
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tlidx, cell.data(), cell.size() * 2);
+            // the values (and the value-update gather map) in the kernel's per-chunk order (spmm_mfma.hpp: 16-byte
+            // entry loads); the cells stay in entry order
+            std::vector<int32_t> tpm(tp.perm.size(), -1);
+            {
+                std::vector<char> tvp(tval.size(), 0);
+                for (size_t ci = 0; ci + 1 < tp.chunks.size(); ++ci) {
+                    const int z = tp.chunks[ci].z, ne = tp.chunks[ci + 1].z - z;
+                    for (int q = 0; q < ne; ++q) {
+                        const int pos = h->vsize == 8 ? mfma_val_pos<double>(q, ne / 8) : mfma_val_pos<float>(q, ne / 8);
+                        std::memcpy(&tvp[(size_t)(z + pos) * h->vsize], &tval[(size_t)(z + q) * h->vsize], h->vsize);
+                        tpm[(size_t)(z + pos)] = (int32_t)tp.perm[(size_t)(z + q)];
+                    }
+                }
+                tval.swap(tvp);
+            }
             if (e == hipSuccess) e = alloc_copy(&h->d_tval, tval.data(), tval.size());
-            std::vector<int32_t> tpm(tp.perm.begin(), tp.perm.end());
             h->ntperm = (int64_t)tpm.size();
             if (e == hipSuccess) e = alloc_copy((void **)&h->d_tperm, tpm.data(), tpm.size() * 4);
             h->insp_bytes += tp.tiles.size() * sizeof(int4) + tp.chunks.size() * sizeof(int4) + tcolT.size() * 4 +

@@ -45,7 +45,12 @@
 //   tiles[t]   = {first C row, rows (<= 16), first chunk, chunks}
 //   tchunk[c]  = {-, columns U, first entry, -}; sentinel after the last chunk
 //   tcolT[c*48 + g*12 + s] = B row of chunk c's union column 4s + g (padded with a valid row past U)
-//   tval[e]    = chunk entries, row by row (padding +0);  tpos[e] = panel cell row * 49 + column (padding: trash)
+//   tpos[e]    = panel cell (row * 49 + column; padding: trash) of the chunk's entry e, row by row; a chunk holds a
+//                multiple of 8 entries (ne = 8 nl) and lane l < nl takes entries 8l .. 8l+7 with ONE 16-byte load
+//   tval[...]  = their values (padding +0), permuted within the chunk so that lane l's 8 values are 16-byte pieces
+//                of 16/sizeof(T)-entry runs: entry 8l + j sits at mfma_val_pos<T>(8l + j, nl) (2 / 4 loads per lane,
+//                fp64 / fp32, each wave instruction contiguous) -- 5 (fp64) or 3 (fp32) vector-memory instructions per
+//                chunk for the entries instead of 16 (the TA issue rate, not bytes, bounds them: r05e PMC)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -62,6 +67,14 @@ constexpr int MFMA_TRASH = MFMA_ROWS * MFMA_PST;
 constexpr int MFMA_PSZ = MFMA_TRASH + 2;       // one wave's panel (+ trash cell)
 constexpr int MFMA_CAPA = 512;                 // entries per chunk (8 per lane)
 constexpr int MFMA_NPE = MFMA_CAPA / 64;
+
+// Position of chunk entry s (lane s / 8, its j = s % 8) in the chunk's value block of 8 nl entries (see tval above)
+template <typename T>
+__host__ __device__ inline int mfma_val_pos(int s, int nl) {
+    constexpr int VPL = 16 / (int)sizeof(T);
+    const int l = s >> 3, j = s & 7;
+    return VPL * nl * (j / VPL) + VPL * l + (j % VPL);
+}
 
 // Per value type: the 16x16x4 MFMA, its accumulator, the B operand piece a lane loads (columns 2j, 2j+1 of a
 // 32-column sub-panel: 16 B fp64 / 8 B fp32), the C/D row map (f64: row = g + 4i; f32: row = 4g + i, g = lane >> 4 --
@@ -133,8 +146,11 @@ __global__ __launch_bounds__(256, (mfma_waves<T, NP, R>())) void spmm_mfma_tile_
     bop_t bo[NP][R];
     int tcn[MFMA_KS];       // R = 12: union columns of the chunk whose B operand is being loaded (c+1 in iteration c)
     int tn = 0;             // lane < 48: one union column of chunk c+2, fetched an iteration ahead
-    T ev[MFMA_NPE];
-    int ep[MFMA_NPE], hc[MFMA_NPE];
+    constexpr int VPL = 16 / (int)sizeof(T);     // values per 16-byte piece
+    typedef T tv __attribute__((ext_vector_type(VPL)));
+    tv ev[8 / VPL];                              // this lane's 8 entries: values ...
+    i32x4 ep;                                    // ... and panel cells (8 x u16)
+    int hc[8];
     int ne = 0;
     // Vector-memory results are waited for in issue order (s_waitcnt vmcnt): a wait for one load drags every older load
     // with it, and the compiler's waits are static, sized for every path into a block.  So a register the loop's B
@@ -167,21 +183,21 @@ __global__ __launch_bounds__(256, (mfma_waves<T, NP, R>())) void spmm_mfma_tile_
 #pragma unroll
         for (int p = 0; p < NP; ++p) bo[p][st % R] = M::load(rs, (uint32_t)col * ldb + lane_off + SUB * p);
     };
-    auto load_e = [&](int c) {
+    auto load_e = [&](int c) {                    // 16-byte loads only (lanes past the entries reload the last 8)
         const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
         ne = cn.z - ch.z;
+        const int nl = ne >> 3, lq = min(l, nl - 1);
+        ep = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(tpos + ch.z) + lq);
 #pragma unroll
-        for (int j = 0; j < MFMA_NPE; ++j) {
-            const int e = min(j * 64 + l, ne - 1);
-            ev[j] = __builtin_nontemporal_load(tval + ch.z + e);
-            ep[j] = (int)__builtin_nontemporal_load(tpos + ch.z + e);
-        }
+        for (int q = 0; q < 8 / VPL; ++q)
+            ev[q] = __builtin_nontemporal_load(reinterpret_cast<const tv *>(tval + ch.z + VPL * nl * q) + lq);
     };
     auto scatter = [&]() {
+        const bool on = 8 * l < ne;
 #pragma unroll
-        for (int j = 0; j < MFMA_NPE; ++j) {
-            const int cell = j * 64 + l < ne ? ep[j] : MFMA_TRASH;
-            P[cell] = ev[j];
+        for (int j = 0; j < 8; ++j) {
+            const int cell = on ? (int)((uint32_t)ep[j >> 1] >> (16 * (j & 1)) & 0xFFFFu) : MFMA_TRASH;
+            P[cell] = ev[j / VPL][j % VPL];
             hc[j] = cell;
         }
     };
@@ -206,7 +222,7 @@ __global__ __launch_bounds__(256, (mfma_waves<T, NP, R>())) void spmm_mfma_tile_
 #pragma unroll
         for (int st = 0; st < MFMA_KS; ++st) a[st] = pa[4 * st];
 #pragma unroll
-        for (int j = 0; j < MFMA_NPE; ++j) P[hc[j]] = T(0);
+        for (int j = 0; j < 8; ++j) P[hc[j]] = T(0);
         if (c + 1 < tl.w) scatter();             // chunk c+1's entries (ev / ep, loaded an iteration ago) ...
         load_e(min(c + 2, tl.w - 1));             // ... before the registers take chunk c+2's
 #pragma unroll
@@ -291,12 +307,13 @@ __global__ __launch_bounds__(256) void mfma_fixup_kernel(
             for (int i = 0; i < 8; ++i) x[i] = T(0);
             for (int c = 0; c < tl.w; ++c) {
                 const int4 ch = tchunk[tl.z + c], cn = tchunk[tl.z + c + 1];
+                const int nl = (cn.z - ch.z) >> 3;
                 for (int e = ch.z; e < cn.z; ++e) {
                     const int cell = (int)tpos[e];
                     const int r = cell / MFMA_PST, k = cell % MFMA_PST;
                     if (cell == MFMA_TRASH || !M::owns(r, g)) continue;
                     const int row = tcolT[(size_t)(tl.z + c) * MFMA_UC + (k & 3) * MFMA_KS + (k >> 2)];
-                    const T av = tval[e];
+                    const T av = tval[ch.z + mfma_val_pos<T>(e - ch.z, nl)];
                     const T *b = B + (size_t)row * ld + k0 + c0;
 #pragma unroll
                     for (int q = 0; q < 4; ++q)

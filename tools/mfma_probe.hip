@@ -1,4 +1,6 @@
-// tools/mfma_probe.hip -- measurement-only C ABI over spmm_mfma_tile_kernel, driven by
+// tools/mfma_probe.hip -- measurement-only C ABI over spmm_mfma_tile_kernel (round-3/4 measurements: its host
+// tables are the round-4 entry layout -- since round 5 the engine permutes each chunk's values, so rebuild this probe only
+// against the round-4 header, git show ff75116~1:spmm-research_amd/csrc/spmm_mfma.hpp), driven by
 // tools/mfma_probe.py with tile tables from spmm_hip_debug_tiles, before the kernel is wired into the engine.
 //   hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/mfma_probe.hip -o spmm-research_amd/lib/libmfma_probe.so
 #include <hip/hip_runtime.h>
