@@ -269,7 +269,8 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
 /* Diagnostics (host only): the matrix-core gate's cost model on a recorded sample -- sample[7] =
  * {tiles sampled, mean reuse, fraction taken, est. taken tiles, est. nonzeros in them, est. chunks, largest sampled
  * chunk count} as spmm_hip_debug_plan reports them ([9], [2], [3], [26], [4], [5], [6]), kw its K-panel width
- * ([12]), dtype the value type (its constant set); out[3] = {verdict, model
+ * ([12]), dtype the value type (its constant set); the matrix is taken as square (ncols = m, as every dataset
+ * line); out[3] = {verdict, model
  * time with matrix-core tiles (us), without (us)}.  Lets a census re-decide with this library's constants without
  * regenerating the matrices (tools/plan_census.py --regate). */
 int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, int32_t dtype, const double *sample,

@@ -1019,21 +1019,21 @@ double tile_reuse_sample(const int32_t *rp, const int32_t *col, int64_t m, int64
 // (reuse >= MFMA_TILE_REUSE) scaled to the matrix give the work of the tile kernel and of the row kernel on the same
 // rows, priced by mfma_cost (measured constants).
 constexpr int MFMA_GATE_SAMPLE = 256;
-// The tile kernel's cost model (us; fitted on same-process A/B data: tools/fit_mfma_gate.py on 598 medium-dataset
-// (line, K) pairs with the gate forced open, profiles/r04/s_c/).  Per 32-column sub-panel the tile
-// kernel streams each chunk's B rows and MFMAs at a chip-wide rate (MFMA_US_CHUNK per chunk, MFMA_US_TILE per tile for
-// its prologue / epilogue) unless it has too few tiles to fill the chip, when the longest tile's chunk chain bounds it
-// (MFMA_US_CHAIN per chunk).  The row kernel gathers one B row per nonzero per sub-panel (ROW_US_NNZ, cheaper for
-// similar rows -- L2 hits -- and for unpanelled launches that read A once for all columns) plus a per-row cost (C
-// store, row setup).  The tile-kernel constants are the fit's times 0.9: the exact-range check left the MFMA loop
-// afterwards (nochk / checked = 0.88-0.89, profiles/r04/s_b/kt.log).  A tile is taken when it brings at least
-// MFMA_TILE_NPC nonzeros per chunk; a matrix takes matrix-core tiles when they hold MFMA_MIN_TILE_FRAC of its
-// nonzeros and the model's time with them (tiles beside the leftover rows) beats the row kernel's by MFMA_MIN_GAIN.
+// The cost model (us; GateModel below, fitted on same-process A/B data by tools/fit_mfma_gate.py, DESIGN §6.18,
+// §6.22).  Per 32-column sub-panel the tile kernel streams each chunk's B rows and MFMAs at a chip-wide rate
+// (us_chunk per chunk, us_tile per tile for its prologue / epilogue) unless it has too few tiles to fill the chip,
+// when the longest tile's chunk chain bounds it (us_chain per chunk); each launch also checks B's exact range (us_bmb
+// per MB of B).  The row kernel gathers one B row per nonzero per sub-panel (row_nnz, cheaper for similar rows -- L2
+// hits -- and for unpanelled launches that read A once for all columns) plus a per-row cost (C store, row setup).  A
+// tile is taken when it brings at least `npc` nonzeros per chunk; a matrix takes matrix-core tiles when they hold
+// min_tile_frac of its nonzeros and the model's time with them (tiles beside the leftover rows) beats the row
+// kernel's by min_gain.
 // One constant set per value type (the matrix-core tile kernel, its B operand and the row kernel's gather all differ
 // in width between fp64 and fp32).  `on` = false: the default policy never takes matrix-core tiles for that type
 // (SPMM_HIP_MFMA >= 1 still does).
 struct GateModel {
     double us_chunk, us_tile, us_chain, us_launch;     // tile kernel
+    double us_bmb;           // + the per-launch exact-range check of B, per MB of B
     double row_launch, row_nnz, row_reuse_exp, row_kw_exp, row_row;   // row kernel
     double npc;              // nonzeros per chunk for a tile to be taken (MFMA_TILE_NPC)
     double min_tile_frac;    // taken tiles must hold this share of the nonzeros
@@ -1041,15 +1041,16 @@ struct GateModel {
     double k32_min_row_nnz;  // one 32-column sub-panel (K < 64): rows must average this many nonzeros
     bool on;
 };
-// fp64: round-4 fit (598 pairs, profiles/r04/s_c/), tile constants x 0.9 (the range check left the MFMA loop);
-// K < 64 rule: the changed-lines sweep of the round-4 census measured avg-10 / avg-20 lines at K = 32 at 0.79x /
-// 0.95x (median, one worker alone on the GPU) where the model predicted 1.38 / 1.37.
-constexpr GateModel GATE_F64 = {1.385e-3, 1.36e-3, 1.01, 22.0, 7.2, 1.877e-5, 0.148, 0.200, 7.05e-5,
-                                96.0, 0.9, 1.30, 32.0, true};
-// fp32: not fitted yet -- the fp64 constants, and off under the default policy (three fp32 twins ran
-// 0.88-0.94x with fp64-fitted tiles)
-constexpr GateModel GATE_F32 = {1.385e-3, 1.36e-3, 1.01, 22.0, 7.2, 1.877e-5, 0.148, 0.200, 7.05e-5,
-                                96.0, 0.9, 1.30, 32.0, false};
+// Round-5 fits (tools/fit_mfma_gate.py on same-process A/B of the gate forced open against no matrix-core tiles, the
+// round-5 tile kernel, 168 lines x K 32 / 128 per type, profiles/r05/fit/).  Rule per type from the
+// fit sample: taken tiles hold >= 90 % of the nonzeros and the model gains >= 1.2x (fp64: 48 pairs taken, worst
+// 1.05x, aggregate 1.11x; fp32: 36 taken, worst 1.00x, aggregate 1.06x).  K < 64 rule (rows averaging < 32
+// nonzeros keep the row kernel at one 32-column sub-panel): the round-4 changed-lines sweep measured avg-10 / avg-20
+// lines at K = 32 at 0.79x / 0.95x alone on the GPU.
+constexpr GateModel GATE_F64 = {0.001271, 0.001405, 0.9645, 27.58, 0.1616, 6.283, 1.582e-05,
+                                0.04599, 0.2127, 7.99e-05, 96.0, 0.9, 1.2, 32.0, true};
+constexpr GateModel GATE_F32 = {0.0007035, 0.0, 0.6146, 31.06, 0.519, 6.935, 7.987e-06,
+                                -0.0298, 0.1672, 3.012e-05, 96.0, 0.9, 1.2, 32.0, true};
 inline const GateModel &gate_model(size_t vsize) { return vsize == 8 ? GATE_F64 : GATE_F32; }
 constexpr int64_t MFMA_GATE_MIN_NNZ = 500000;
 struct MfmaGate {
@@ -1117,13 +1118,14 @@ MfmaGate mfma_sample(const int32_t *rp, const int32_t *col, int64_t m, int64_t n
 }
 
 // The gate: the cost model above for the K columns in 32-column sub-panels.
-void mfma_cost(MfmaGate &g, int64_t m, int64_t nnz, int k, int kw, const GateModel &c) {
+void mfma_cost(MfmaGate &g, int64_t m, int64_t ncols, int64_t nnz, int k, int kw, size_t vsize, const GateModel &c) {
     const double P = (double)k / 32.0;
     const double r_row = c.row_nnz * std::pow(std::max(g.r16, 1.0), -c.row_reuse_exp) *
                          std::pow((double)std::max(kw, 1) / 32.0, -c.row_kw_exp);
     g.t_off = c.row_launch + P * ((double)nnz * r_row + (double)m * c.row_row);
     const double t_tiles = c.us_launch + P * std::max(g.chunks * c.us_chunk + g.tiles * c.us_tile,
-                                                      g.max_chunks * c.us_chain);
+                                                      g.max_chunks * c.us_chain) +
+                           c.us_bmb * (double)ncols * (double)k * (double)vsize * 1e-6;
     const double left_rows = std::max((double)m - (double)MFMA_ROWS * g.tiles, 0.0);
     const double t_left = c.row_launch + P * (((double)nnz - g.tile_nnz) * r_row + left_rows * c.row_row);
     g.t_on = std::max(t_tiles, t_left);
@@ -1267,7 +1269,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
                 const GateModel &gm = gate_model(h->vsize);
                 const double npc = force_all ? 0.0 : (npc_env && *npc_env) ? atof(npc_env) : gm.npc;
                 d.gate = mfma_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, treuse, npc);
-                mfma_cost(d.gate, h->m, h->nnz, k, pl.kw, gm);
+                mfma_cost(d.gate, h->m, h->ncols, h->nnz, k, pl.kw, h->vsize, gm);
                 pl.tile_reuse = d.gate.r16;
                 if (gate_only) {
                     d.gate_only = true;
@@ -2315,7 +2317,8 @@ int spmm_hip_debug_gate(int64_t m, int64_t nnz, int32_t k, int32_t kw, int32_t d
     g.tile_nnz = sample[4];
     g.chunks = sample[5];
     g.max_chunks = sample[6];
-    mfma_cost(g, m, nnz, k, kw, gate_model(dtype == SPMM_HIP_F64 ? 8 : 4));
+    // (the census's matrices are square: ncols = m)
+    mfma_cost(g, m, m, nnz, k, kw, dtype == SPMM_HIP_F64 ? 8 : 4, gate_model(dtype == SPMM_HIP_F64 ? 8 : 4));
     out[0] = g.verdict;
     out[1] = g.t_on;
     out[2] = g.t_off;

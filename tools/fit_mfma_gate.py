@@ -76,8 +76,10 @@ def model(F, c):
     P = F["k"] / 32.0
     r_row = c["row_us_nnz"] * np.maximum(F["r16"], 1.0) ** -c["row_reuse_exp"] * (F["kw"] / 32.0) ** -c["row_kw_exp"]
     t_off = c["launch"] + P * (F["nnz"] * r_row + F["m"] * c["row_us_row"])
+    # + the per-launch exact-range check of B (one pass over ncols x K values; square dataset matrices: ncols = m)
+    b_mb = F["m"] * F["k"] * F.get("vsize", 8.0) / 1e6
     t_tiles = c["mfma_launch"] + P * np.maximum(F["est_chunks"] * c["us_chunk"] + F["est_tiles"] * c["us_tile"],
-                                                F["max_chunks"] * c["us_chain"])
+                                                F["max_chunks"] * c["us_chain"]) + b_mb * c.get("us_bmb", 0.0)
     left_rows = np.maximum(F["m"] - 16.0 * F["est_tiles"], 0.0)
     t_left = c["launch"] + P * ((F["nnz"] - F["est_tile_nnz"]) * r_row + left_rows * c["row_us_row"])
     return np.maximum(t_tiles, t_left), t_off
@@ -102,21 +104,23 @@ def fit(args):
     keys = [k for k in ab if k in feats and ab[k]["tile_mode"] == "mfma"]
     F = {f: np.array([feats[k][f] if f in feats[k] else ab[k][f] for k in keys], float)
          for f in ("k", "nnz", "m", "est_chunks", "est_tiles", "est_tile_nnz", "max_chunks", "r16", "kw")}
+    F["vsize"] = np.full(len(keys), 8.0 if args.dtype == "f64" else 4.0)
     t_on = np.array([ab[k]["ms"] * 1e3 for k in keys])
     t_off = np.array([ab[k]["ms_base"] * 1e3 for k in keys])
     base = {"min_tile_frac": 0.0, "gain": 1.0}
 
     def c_of(x, y):
         return {**base, "launch": y[0], "row_us_nnz": y[1], "row_reuse_exp": y[2], "row_kw_exp": y[3],
-                "row_us_row": y[4], "mfma_launch": x[0], "us_chunk": x[1], "us_tile": x[2], "us_chain": x[3]}
+                "row_us_row": y[4], "mfma_launch": x[0], "us_chunk": x[1], "us_tile": x[2], "us_chain": x[3],
+                "us_bmb": x[4] if len(x) > 4 else 0.0}
     # the row kernel (every line: the baseline plan has no matrix-core tiles)
-    y = least_squares(lambda y: np.log(model(F, c_of([0, 0, 0, 0], y))[1] / t_off), [5, 2.5e-5, 0.2, 0.15, 1e-4],
+    y = least_squares(lambda y: np.log(model(F, c_of([0, 0, 0, 0, 0], y))[1] / t_off), [5, 2.5e-5, 0.2, 0.15, 1e-4],
                       bounds=([0, 0, -2, -2, 0], [100, 1e-3, 3, 3, 1e-2])).x
     # the tile kernel on the lines whose tiles hold >= 90 % of the nonzeros (t_on is then the tile kernel)
     sel = F["est_tile_nnz"] >= 0.9 * F["nnz"]
     Fs = {k: v[sel] for k, v in F.items()}
-    x = least_squares(lambda x: np.log(model(Fs, c_of(x, y))[0] / t_on[sel]), [20, 1.6e-3, 1.5e-3, 1.1],
-                      bounds=([0, 0, 0, 0], [200, 1e-2, 1e-2, 50]), loss="soft_l1").x
+    x = least_squares(lambda x: np.log(model(Fs, c_of(x, y))[0] / t_on[sel]), [20, 1.6e-3, 1.5e-3, 1.1, 0.2],
+                      bounds=([0, 0, 0, 0, 0], [200, 1e-2, 1e-2, 50, 5]), loss="soft_l1").x
     c = c_of(x, y)
     m_on, m_off = model(F, c)
     print(json.dumps({"fit": {k: float(v) for k, v in c.items()}, "lines": len(keys), "tile_lines": int(sel.sum()),
