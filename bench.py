@@ -366,7 +366,7 @@ def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, 
         b = S.bytes_alg(A.m, A.ncols, A.nnz, K, dt_code)
         rec = {"gen": line, "m": int(A.m), "nnz": int(A.nnz), "ms": t * 1e3, "flops": 2.0 * A.nnz * K,
                "bytes_alg": b, "frac": b / t / 1e9 / HBM_PEAK_GBS, "gflops": 2.0 * A.nnz * K / t / 1e9,
-               "tiles": int(mf.info()[19]), "selfcheck_ok": chk["ok"]}
+               "tiles": int(mf.info()[19]), "tile_mode": mf.tile_info()["mode"], "selfcheck_ok": chk["ok"]}
         if names:
             rec["name"] = names.get(line)
         pm = pmc.get(line)
@@ -482,7 +482,8 @@ def run_twins(args, torch, S, np):
         s = summarize(res, args.k)
         s["per_twin"] = [{"name": r["name"], "nnz": r["nnz"], "ms": round(r["ms"], 5), "gflops": round(r["gflops"], 1),
                           "frac": round(r["frac"], 4), "cpu_gflops": round(r["flops"] / r["cpu_ms"] / 1e6, 2)
-                          if r.get("cpu_ms") else None, "tiles": r["tiles"]} for r in res["recs"]]
+                          if r.get("cpu_ms") else None, "tiles": r["tiles"], "tile_mode": r["tile_mode"]}
+                         for r in res["recs"]]
         bad += res["bad"]
         per[dt] = s
     line = {"metric": "GFLOP/s, validation twins (config 5), CSR SpMM K=32, aggregate over the twins",
