@@ -6,7 +6,7 @@
 # 32 sampled rows against the oracle (bit-exact on exact rows, 1e-10 normwise + fp128 gold on the rest).
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
-BUDGET=${1:-900}; WORKERS=${2:-12}; NAME=r05_sweep_medium
+BUDGET=${1:-900}; WORKERS=${2:-8}; NAME=r05_sweep_medium
 OUT=gpurun_out/sweep; mkdir -p $OUT
 export TMPDIR=/tmp OMP_NUM_THREADS=2
 STAMP=$(date +%s)
