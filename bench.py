@@ -201,9 +201,9 @@ def achievable(t_ms: float, traffic: float | None, l2_req: float | None, b_bytes
             "frac_of_achievable": round(t / t_ms, 4)}
 
 
-def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
+def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype):
     """The reference compute_csr (restated in oracle/spmm_oracle.c, bit-pinned against the reference build) on this
-    host, same A and the same column-major x the GPU's B was made from."""
+    host, same A and the same column-major x the GPU's B was made from: (the oracle's C [m][k], the record)."""
     import numpy as np
     from oracle import oracle as O
     threads, model = cpu_share()
@@ -234,6 +234,7 @@ def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
     times.sort()
     t = times[len(times) // 2]
     gf = 2.0 * A.nnz * k / t / 1e9
+    y_x = y.reshape(A.m, k).copy()             # the oracle's C for this x: the caller checks the GPU's C against it
     # the reference harness's own B (x = 1.0, spmv_bench.cpp:901) as well: BASELINE.md asks for both
     ones = np.ones_like(x)
     fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, ones, y, k, threads)
@@ -243,7 +244,7 @@ def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
         fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, ones, y, k, threads)
         t1.append(time.perf_counter() - t0)
     t_ones = sorted(t1)[2]
-    return {"value": round(gf, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+    return y_x, {"value": round(gf, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
             "value_x_ones": round(2.0 * A.nnz * k / t_ones / 1e9, 3),
             "sample": (f"full matrix, same A and x (drand48 seed 42, column-major) as the GPU run; oracle/liboracle.so "
                        f"(C restatement of compute_csr, bit-identical to the reference build); {threads} OpenMP threads "
@@ -252,8 +253,9 @@ def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype) -> dict:
                        f"reference harness's x = 1.0, 5 timed calls, median {t_ones * 1e3:.1f} ms/call")}
 
 
-def cpu_time_once(A, x_col, k: int, dtype, threads: int, budget_s: float) -> float:
-    """One warm-up + timed calls of the oracle's compute_csr within budget_s (at least one); median seconds."""
+def cpu_time_once(A, x_col, k: int, dtype, threads: int, budget_s: float):
+    """One warm-up + timed calls of the oracle's compute_csr within budget_s (at least one): (median seconds, the
+    oracle's C [m][k], which the caller checks the GPU's C against)."""
     import numpy as np
     from oracle import oracle as O
     L = O.lib()
@@ -267,7 +269,33 @@ def cpu_time_once(A, x_col, k: int, dtype, threads: int, budget_s: float) -> flo
         t0 = time.perf_counter()
         fn(A.row_ptr, A.col_idx, vals, A.m, A.ncols, x_col, y, k, threads)
         ts.append(time.perf_counter() - t0)
-    return sorted(ts)[len(ts) // 2]
+    return sorted(ts)[len(ts) // 2], y[: A.m * k].reshape(A.m, k)
+
+
+def oracle_compare(A, x_col, k: int, got, want, exact, dtype) -> dict:
+    """The GPU's C against the oracle's C on the same A and B: rows the engine reports exact (one left-to-right FMA
+    chain) must be bit-identical; the rest (split / vector-lane rows) within the normwise contract of SURVEY §8a(ii)
+    (|C - C_ref| <= tol * sum_j |a_ij b_jn|, tol 1e-10 fp64 / (len + 1) 2^-24 fp32, doubled: both sides round)."""
+    import numpy as np
+    iv = np.int64 if got.dtype == np.float64 else np.int32
+    same = (np.ascontiguousarray(got).view(iv) == np.ascontiguousarray(want).view(iv)).all(axis=1)
+    ex = exact[: A.m].astype(bool)
+    out = {"rows_exact": int(ex.sum()), "exact_mismatch": int((ex & ~same).sum()), "rows_inexact": int((~ex).sum()),
+           "inexact_outside_tol": 0}
+    rows = np.flatnonzero(~ex)
+    if len(rows):
+        import scipy.sparse as sp
+        absB = np.abs(np.asarray(x_col, np.float64).reshape(k, A.ncols).T)      # column-major x -> B [ncols][k]
+        absA = sp.csr_matrix((np.abs(A.values.astype(dtype).astype(np.float64)), A.col_idx, A.row_ptr),
+                             shape=(A.m, A.ncols))[rows]
+        absdot = np.asarray(absA @ absB)
+        lens = np.diff(A.row_ptr)[rows].astype(np.float64)
+        tol = np.full(len(rows), 1e-10) if dtype == np.float64 else (lens + 1.0) * 2.0 ** -24
+        d = np.abs(got[rows].astype(np.float64) - want[rows].astype(np.float64))
+        ok_rows = np.all(d <= 2.0 * tol[:, None] * absdot + 1e-300, axis=1)
+        out["inexact_outside_tol"] = int((~ok_rows).sum())
+    out["ok"] = out["exact_mismatch"] == 0 and out["inexact_outside_tol"] == 0
+    return out
 
 
 def selfcheck(A, B_host_rowmajor, C_dev, k: int, dtype, nsample: int = 256, seed: int = 5) -> dict:
@@ -377,8 +405,11 @@ def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, 
         if (cpu_left > 0 or cpu_each_s > 0) and A.nnz > 0:
             t0 = time.perf_counter()
             x_col = np.ascontiguousarray(B.t().cpu().numpy()).ravel()[: A.ncols * K]
-            tc = cpu_time_once(A, x_col, K, npdt, threads, cpu_each_s if cpu_each_s > 0 else min(cpu_left, 2.0))
+            tc, want = cpu_time_once(A, x_col, K, npdt, threads, cpu_each_s if cpu_each_s > 0 else min(cpu_left, 2.0))
             rec["cpu_ms"] = tc * 1e3
+            # the CPU baseline's own output checks this run's C: bit-exact on the rows the engine reports exact
+            rec["oracle_check"] = oracle_compare(A, x_col, K, C[: A.m].cpu().numpy(), want, mf.exact_rows(), npdt)
+            bad += 0 if rec["oracle_check"]["ok"] else 1
             cpu_left -= time.perf_counter() - t0
             del x_col
         recs.append(rec)
@@ -434,6 +465,14 @@ def summarize(res: dict, K: int) -> dict:
                        f"{cf / gs / 1e9:.1f} GFLOP/s")}
     else:
         out["cpu_baseline"] = None
+    oc = [r["oracle_check"] for r in recs if "oracle_check" in r]
+    out["oracle_check"] = {
+        "matrices": len(oc), "rows_exact": sum(c["rows_exact"] for c in oc),
+        "exact_rows_not_bitexact": sum(c["exact_mismatch"] for c in oc),
+        "rows_inexact": sum(c["rows_inexact"] for c in oc),
+        "inexact_rows_outside_tol": sum(c["inexact_outside_tol"] for c in oc),
+        "note": ("every row of the CPU-baselined matrices against the oracle's C on the same A and B: bit-identical "
+                 "where the engine reports the row exact, else within 2x the normwise tolerance")} if oc else None
     return out
 
 
@@ -850,7 +889,11 @@ def main():
     cpu = None
     if rank == 0 and N == 1 and args.workload == "config2" and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(A, x_col, K, args.cpu_warmup, args.cpu_seconds, npdtype)
+            want, cpu = cpu_baseline(A, x_col, K, args.cpu_warmup, args.cpu_seconds, npdtype)
+            # the baseline's own C checks this run's C over every row (bit-exact where the engine reports exact)
+            cpu["oracle_check"] = oracle_compare(A, x_col, K, C[: A.m].cpu().numpy(), want, exact, npdtype)
+            ok_all = ok_all and cpu["oracle_check"]["ok"]
+            del want
         except Exception as e:  # the baseline is reported, never required
             cpu = {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
     mf.close()

@@ -49,3 +49,28 @@ def test_summarize_aggregates():
     assert s["roofline"]["achieved"] == pytest.approx(2000.0)  # sum bytes / sum time
     assert s["roofline"]["traffic"] == 3e9 and s["roofline"]["achievable"]["matrices"] == 1
     assert s["cpu_baseline"]["value"] == pytest.approx(20.0) and "1 of the 2" in s["cpu_baseline"]["sample"]
+
+
+def test_oracle_compare_bitexact_rows_and_tolerance():
+    """The dataset leg's check of the GPU's C against the CPU baseline's oracle output: exact rows must match bit
+    for bit, the others within the normwise contract."""
+    import numpy as np
+    import spmm_amd as S
+    from oracle import oracle as O
+    A = S.generate(S.gen_params("300 300 20 5 normal random 0.3 0 0.5 0.5 14"))
+    k = 4
+    x = O.drand48(3, A.ncols * k) - 0.5
+    want = O.spmm(A.row_ptr, A.col_idx, A.values, A.ncols, x, k)
+    ex = np.ones(A.m, np.uint8)
+    r = bench.oracle_compare(A, x, k, want.copy(), want, ex, np.float64)
+    assert r["ok"] and r["rows_exact"] == A.m and r["exact_mismatch"] == 0
+    got = want.copy()
+    got[3, 1] = np.nextafter(got[3, 1], np.inf)                 # one ulp off on an exact row: a failure
+    r = bench.oracle_compare(A, x, k, got, want, ex, np.float64)
+    assert not r["ok"] and r["exact_mismatch"] == 1
+    ex[3] = 0                                                    # the same row reported inexact: within tolerance
+    r = bench.oracle_compare(A, x, k, got, want, ex, np.float64)
+    assert r["ok"] and r["rows_inexact"] == 1
+    got[3, 1] += 1.0                                             # far off: outside it
+    r = bench.oracle_compare(A, x, k, got, want, ex, np.float64)
+    assert not r["ok"] and r["inexact_outside_tol"] == 1
