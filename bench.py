@@ -499,7 +499,7 @@ def run_medium_sample(args, torch, S, np):
             "higher_is_better": True, "scaling": "single-gpu", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (own generator, seeded; A values U[0.5,1.5), B torch.rand(seed 42))",
             "config": {"workload": "medium-sample: " + d["workload"], "k": args.k, "parallelism": "single-gpu"},
-            "roofline": d["roofline"], "cpu_baseline": d["cpu_baseline"],
+            "roofline": d["roofline"], "cpu_baseline": d["cpu_baseline"], "oracle_check": d.get("oracle_check"),
             "setup": {"wall_s": d["wall_s"], "selfcheck_failures": d["selfcheck_failures"]}}
     print(json.dumps(line), flush=True)
     return 0 if d["selfcheck_failures"] == 0 else 1
@@ -521,7 +521,8 @@ def run_twins(args, torch, S, np):
         s = summarize(res, args.k)
         s["per_twin"] = [{"name": r["name"], "nnz": r["nnz"], "ms": round(r["ms"], 5), "gflops": round(r["gflops"], 1),
                           "frac": round(r["frac"], 4), "cpu_gflops": round(r["flops"] / r["cpu_ms"] / 1e6, 2)
-                          if r.get("cpu_ms") else None, "tiles": r["tiles"], "tile_mode": r["tile_mode"]}
+                          if r.get("cpu_ms") else None, "tiles": r["tiles"], "tile_mode": r["tile_mode"],
+                          "oracle_ok": r["oracle_check"]["ok"] if "oracle_check" in r else None}
                          for r in res["recs"]]
         bad += res["bad"]
         per[dt] = s

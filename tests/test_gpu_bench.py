@@ -72,3 +72,17 @@ def test_bench_medium_sample_record():
     assert 0 < rl["p10_frac"] <= rl["median_frac"] <= rl["p90_frac"] < 1.5
     cb = r["cpu_baseline"]
     assert cb is not None and cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
+    oc = r["oracle_check"]                                   # the CPU leg's oracle C checked this run's C
+    assert oc is not None and oc["matrices"] >= 1 and oc["rows_exact"] > 0
+    assert oc["exact_rows_not_bitexact"] == 0 and oc["inexact_rows_outside_tol"] == 0
+
+
+def test_bench_config2_checked_against_cpu_baseline():
+    """The headline line on a reduced config-2-shaped matrix: its CPU baseline's C (the oracle on the same A and B)
+    checks the GPU's C on every row -- bit-identical rows where the engine reports exact."""
+    r = _bench(["--workload", "config2", "--gen", "100000 100000 20 6.6667 normal random 0.05 0 0.5 0.5 14",
+                "--steps", "3", "--warmup", "1", "--no-dataset", "--no-multi-handle", "--cpu-warmup", "2",
+                "--cpu-seconds", "1"])
+    oc = r["cpu_baseline"]["oracle_check"]
+    assert oc["ok"] and oc["rows_exact"] == 100000 and oc["exact_mismatch"] == 0
+    assert r["setup"]["selfcheck_all_ranks_ok"] is True
