@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--k", default="32")
     ap.add_argument("--plans", default="policy:;off:SPMM_HIP_MFMA=-1")
     ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--repeat", type=int, default=1, help="timed rounds per (line, K, plan), each on a fresh handle")
     args = ap.parse_args()
     import torch
     import spmm_amd as S
@@ -35,12 +37,14 @@ def main():
     for line in args.lines.split(";"):
         A = S.generate(S.gen_params(line))
         for k in (int(x) for x in args.k.split(",")):
-            B = torch.rand((A.ncols, k), device=dev, dtype=torch.float64)
-            C = torch.empty((A.m, k), device=dev, dtype=torch.float64)
-            for name, env in plans:
+            tdt = torch.float64 if args.dtype == "f64" else torch.float32
+            vals = A.values if args.dtype == "f64" else A.values.astype("float32")
+            B = torch.rand((A.ncols, k), device=dev, dtype=tdt)
+            C = torch.empty((A.m, k), device=dev, dtype=tdt)
+            for name, env in [p for p in plans for _ in range(args.repeat)]:
                 old = {kk: os.environ.get(kk) for kk in env}
                 os.environ.update(env)
-                mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values, A.m, A.ncols, A.nnz, k, 0)
+                mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, k, 0)
                 for _ in range(3):
                     mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), k, st.cuda_stream)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,7 +59,7 @@ def main():
                     else:
                         os.environ[kk] = vv
                 inf = mf.info()
-                print(json.dumps({"gen": line, "k": k, "plan": name,
+                print(json.dumps({"gen": line, "k": k, "plan": name, "dtype": args.dtype,
                                   "ms": round(e0.elapsed_time(e1) / args.launches, 5),
                                   "tile": mf.tile_info(), "info": [int(v) for v in inf]}), flush=True)
                 mf.close()

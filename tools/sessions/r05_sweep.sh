@@ -11,6 +11,6 @@ OUT=gpurun_out/sweep; mkdir -p $OUT
 export TMPDIR=/tmp OMP_NUM_THREADS=2
 STAMP=$(date +%s)
 timeout -k 10 $((BUDGET + 240)) python -u tools/sweep.py --order interleave16 --k 1,8,32,128 --budget $BUDGET \
-    --workers $WORKERS --no-features --check-rows 32 --gold-rows 16 --iters 10 --done profiles/$NAME.done \
+    --workers $WORKERS --lock-alloc --no-features --check-rows 32 --gold-rows 16 --iters 10 --done profiles/$NAME.done \
     --out $OUT/$NAME.$STAMP.jsonl > $OUT/$NAME.$STAMP.log 2>&1
 rc=$?; tail -n 2 $OUT/$NAME.$STAMP.log | cut -c1-200; cat $OUT/$NAME.$STAMP*.jsonl | wc -l; exit $rc

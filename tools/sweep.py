@@ -227,6 +227,11 @@ def main():
     ap.add_argument("--workers", type=int, default=1, help="host worker processes (timed regions serialised)")
     ap.add_argument("--worker", default=None, help=argparse.SUPPRESS)     # i/W: set by --workers
     ap.add_argument("--gpu-lock", default=None, help="lock file serialising the timed regions of the workers")
+    ap.add_argument("--lock-alloc", action="store_true",
+                    help="also hold the GPU lock while a worker uploads A, allocates and fills B and C, and frees them: "
+                         "another worker's large allocations, fills and frees stretched a timed region by up to 2-3x "
+                         "on K=128 lines of > 10 M nonzeros (round 5); only the planner's host work and the checks "
+                         "then overlap a timed region")
     ap.add_argument("--env", default="", help="ENV=V,ENV=V set while the engine plans (e.g. SPMM_HIP_MFMA=2)")
     ap.add_argument("--base-env", default=None,
                     help="A/B: also plan a baseline handle with these ENV=V,... (e.g. SPMM_HIP_MFMA=-1: the plan without "
@@ -345,8 +350,13 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
         tdtype = torch.float64 if dt == "f64" else torch.float32
         vals = A.values.astype(dtype)
         tc = time.time()
+        if lock_f and args.lock_alloc:
+            fcntl.flock(lock_f, fcntl.LOCK_EX)
         mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
         mfb = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0) if args.base_env is not None else None
+        torch.cuda.synchronize()
+        if lock_f and args.lock_alloc:
+            fcntl.flock(lock_f, fcntl.LOCK_UN)
         t_create = time.time() - tc
         for dt2, k in todo:
             if dt2 != dt:
@@ -358,6 +368,8 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
             if mfb is not None:
                 with env_set(args.base_env):
                     mfb.plan(k)
+            if lock_f and args.lock_alloc:
+                fcntl.flock(lock_f, fcntl.LOCK_EX)
             g = torch.Generator(device=dev)
             g.manual_seed(42)
             B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
@@ -368,7 +380,7 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
                 Cb = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
                 runb = lambda: mfb.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cb.data_ptr(), k, stream.cuda_stream)  # noqa
             torch.cuda.synchronize()
-            if lock_f:
+            if lock_f and not args.lock_alloc:
                 fcntl.flock(lock_f, fcntl.LOCK_EX)
 
             def timed(fn):
@@ -434,10 +446,21 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
             print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
                                                          "roofline_frac", "cpu_gflops", "speedup", "bitexact_seq_rows",
                                                          "normwise_ok")}), flush=True)
+            if lock_f and args.lock_alloc:
+                fcntl.flock(lock_f, fcntl.LOCK_EX)
             del B, Cm, Cb
+            torch.cuda.synchronize()
+            if args.worker is not None:
+                torch.cuda.empty_cache()
+            if lock_f and args.lock_alloc:
+                fcntl.flock(lock_f, fcntl.LOCK_UN)
+        if lock_f and args.lock_alloc:
+            fcntl.flock(lock_f, fcntl.LOCK_EX)
         mf.close()
         if mfb is not None:
             mfb.close()
+        if lock_f and args.lock_alloc:
+            fcntl.flock(lock_f, fcntl.LOCK_UN)
 
 
 if __name__ == "__main__":
