@@ -8,7 +8,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 BUDGET=${1:-900}; WORKERS=${2:-8}; NAME=r05_sweep_medium
 OUT=gpurun_out/sweep; mkdir -p $OUT
-export TMPDIR=/tmp OMP_NUM_THREADS=2
+export TMPDIR=/tmp OMP_NUM_THREADS=${SWEEP_OMP:-2}
 STAMP=$(date +%s)
 timeout -k 10 $((BUDGET + 240)) python -u tools/sweep.py --order interleave16 --k 1,8,32,128 --budget $BUDGET \
     --workers $WORKERS --lock-alloc --no-features --check-rows 32 --gold-rows 16 --iters 10 --done profiles/$NAME.done \
