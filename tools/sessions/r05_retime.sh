@@ -2,7 +2,7 @@
 # round 5: re-time the config-3 records flagged by tools/sweep_flag.py (timed regions stretched by other workers),
 # one K per pass so every worker runs the same kind of launch (the configuration in which the contamination probe,
 # tools/sessions/r05_contam.sh, measured 8 workers as clean as one):
-#   bash tools/sessions/r05_retime.sh <pairs file> <K> <budget_s> <workers>
+#   bash tools/sessions/r05_retime.sh <pairs file> <K list> <budget_s> <workers>
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 PAIRS=$1; K=$2; BUDGET=${3:-900}; WORKERS=${4:-8}; NAME=r05_sweep_medium
