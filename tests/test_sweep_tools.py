@@ -86,3 +86,45 @@ def test_sweep_done_pairs_and_changed_pairs(tmp_path):
     tool = Path(__file__).resolve().parents[1] / "tools" / "sweep_done_pairs.py"
     subprocess.run([sys.executable, str(tool), str(rec), "--out", str(out)], check=True, capture_output=True)
     assert out.read_text() == "32\t1 1 1\n"
+
+
+def _gen(avg, bw):
+    return f"1000 1000 {avg} 1 normal random {bw} 0 0.5 0.5 14"
+
+
+def test_sweep_flag_selects_slow_same_plan_and_spread_batches(tmp_path):
+    """tools/sweep_flag.py: a record > 1.3x the reference's same plan is flagged, a faster one or one whose plan
+    changed (tiles) is not; a record whose batches disagree by > 1.25x is flagged on its own."""
+    import json
+    import subprocess
+    plan = {"blocks": 10, "panel_k": 32, "windows": 1, "split_rows": 0, "tiles": 0, "dtype": "f64"}
+    ref = [dict(gen=_gen(20, 0.05), k=128, ms=1.0, **plan), dict(gen=_gen(20, 0.3), k=128, ms=1.0, **plan),
+           dict(gen=_gen(50, 0.05), k=32, ms=1.0, **plan)]
+    new = [dict(gen=_gen(20, 0.05), k=128, ms=2.0, batches=[2.0, 2.0, 2.1], **plan),      # same plan, 2x: flagged
+           dict(gen=_gen(20, 0.3), k=128, ms=0.9, batches=[0.9, 0.95, 0.9], **plan),       # faster: kept
+           dict(gen=_gen(50, 0.05), k=32, ms=2.0, batches=[2.0, 2.0, 2.0], **{**plan, "tiles": 5}),   # tiles: kept
+           dict(gen=_gen(5, 0.6), k=8, ms=1.0, batches=[1.0, 1.6, 1.1], **plan)]           # batch spread: flagged
+    (tmp_path / "ref.jsonl").write_text("".join(json.dumps(r) + "\n" for r in ref))
+    (tmp_path / "new.jsonl").write_text("".join(json.dumps(r) + "\n" for r in new))
+    out = tmp_path / "pairs.txt"
+    tool = Path(__file__).resolve().parents[1] / "tools" / "sweep_flag.py"
+    subprocess.run([sys.executable, str(tool), str(tmp_path / "new.jsonl"), "--ref", str(tmp_path / "ref.jsonl"),
+                    "--out", str(out)], check=True, capture_output=True)
+    assert out.read_text().splitlines() == [f"8\t{_gen(5, 0.6)}", f"128\t{_gen(20, 0.05)}"]
+
+
+def test_sweep_compare_speedups(tmp_path):
+    """tools/sweep_compare.py: per-K geomean of old / new kernel time over the common (line, K) pairs."""
+    import json
+    import subprocess
+    old = [dict(gen=_gen(20, 0.05), k=32, ms=2.0, nnz=20000, roofline_frac=0.1),
+           dict(gen=_gen(500, 0.3), k=32, ms=1.0, nnz=500000, roofline_frac=0.2)]
+    new = [dict(gen=_gen(20, 0.05), k=32, ms=1.0, nnz=20000, roofline_frac=0.2),
+           dict(gen=_gen(500, 0.3), k=32, ms=1.0, nnz=500000, roofline_frac=0.2)]
+    (tmp_path / "o.jsonl").write_text("".join(json.dumps(r) + "\n" for r in old))
+    (tmp_path / "n.jsonl").write_text("".join(json.dumps(r) + "\n" for r in new))
+    tool = Path(__file__).resolve().parents[1] / "tools" / "sweep_compare.py"
+    r = subprocess.run([sys.executable, str(tool), str(tmp_path / "o.jsonl"), str(tmp_path / "n.jsonl")],
+                       check=True, capture_output=True, text=True)
+    row = [l for l in r.stdout.splitlines() if l.startswith("| 32 |")][0]
+    assert "| 2 | 1.414 |" in row                               # sqrt(2 x 1)
