@@ -396,6 +396,7 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
                 if runb is not None:
                     runb()
             ms_b, msb_b = [], []
+            t_wall = time.time()               # wall clock of the timed region (correlation with other activity)
             for _ in range(args.batches):          # baseline and policy interleaved batch by batch
                 if runb is not None:
                     msb_b.append(timed(runb))
@@ -412,7 +413,7 @@ def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock
             rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
                    "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
                    "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9, "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12,
-                   "engine_sha256": sha, "batches": [round(x, 5) for x in ms_b], "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
+                   "engine_sha256": sha, "batches": [round(x, 5) for x in ms_b], "t_wall": round(t_wall, 3), "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
                    "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
                    "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
                    "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]), "tile_mode": mf.tile_info()["mode"],
