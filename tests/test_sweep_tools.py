@@ -128,3 +128,43 @@ def test_sweep_compare_speedups(tmp_path):
                        check=True, capture_output=True, text=True)
     row = [l for l in r.stdout.splitlines() if l.startswith("| 32 |")][0]
     assert "| 2 | 1.414 |" in row                               # sqrt(2 x 1)
+
+
+def test_gpu_rwlock_writer_excludes_readers_and_is_not_starved(tmp_path):
+    """tools/gpu_rwlock.py: readers share; a writer waits for the readers inside, and a reader arriving after the
+    writer waits for it (writer preference) -- checked with three processes and a shared event log."""
+    import multiprocessing as mp
+    import time
+    from gpu_rwlock import GpuRWLock
+    path, log = str(tmp_path / "gpu.lock"), tmp_path / "log.txt"
+
+    def note(s):
+        with open(log, "a") as f:
+            f.write(f"{time.monotonic():.4f} {s}\n")
+
+    def reader(name, delay, hold):
+        time.sleep(delay)
+        lk = GpuRWLock(path)
+        with lk.shared():
+            note(f"{name} in")
+            time.sleep(hold)
+            note(f"{name} out")
+
+    def writer(delay, hold):
+        time.sleep(delay)
+        lk = GpuRWLock(path)
+        with lk.exclusive():
+            note("W in")
+            time.sleep(hold)
+            note("W out")
+
+    ctx = mp.get_context("fork")
+    ps = [ctx.Process(target=reader, args=("R1", 0.0, 0.6)), ctx.Process(target=writer, args=(0.2, 0.4)),
+          ctx.Process(target=reader, args=("R2", 0.4, 0.1))]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(10)
+        assert p.exitcode == 0
+    ev = [l.split(" ", 1)[1] for l in sorted(log.read_text().splitlines())]
+    assert ev == ["R1 in", "R1 out", "W in", "W out", "R2 in", "R2 out"]
