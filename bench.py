@@ -7,24 +7,33 @@ CHILD process (before anything touches the GPU) and exits with its status.  A wo
 is an error (exit 2).  One "step" = one SpMM over the rank's row shard, inputs resident in HBM.  Rank 0 prints ONE
 JSON line.
 
-The line (default, --workload config2):
-  value     config 2 (BASELINE.json configs[1]): generator line
-            1000000 1000000 20 6.6667 normal random 0.3 100 0.95 0.5 14, K=32 fp64; at N > 1 one such matrix per
-            GPU (weak scaling, the default: the path partitions into independent row shards with no collective in the
-            timed step -- every rank owns a config-2-sized nnz-balanced row range of one N-times-larger matrix of the
-            same shape; --scaling strong splits the single config-2 matrix N ways instead).  value = 2*nnz*K*steps /
-            (max over ranks of the HIP-event time of the K timed steps on the launch stream); the
-            barrier-inclusive wall time is reported beside it ("wall_ms_per_step").
-  dataset   (N=1 only; --no-dataset skips it) the metric's own workload, BASELINE "synthetic medium dataset, K=32
-            fp64": every --dataset-stride-th line of synthetic_matrices_medium_dataset (stride 160 = 102 matrices),
-            per matrix `--dataset-iters` HIP-event-timed launches; aggregate GFLOP/s (sum flops / sum time), median /
-            p10 / p90 roofline fraction, per-matrix PMC traffic when profiles/ holds it for this engine build, an
-            achievable-ceiling fraction, and a cpu_baseline on a time-bounded subset of the same matrices (same A and
-            B).  "scaling": "single-gpu".
-Other workloads (N=1 unless noted):
-  config4   (N >= 1) the largest avg-20 skew-10^4 line of synthetic_matrices_large_dataset.txt with gamma row lengths
-            (7477550 rows, 150 M nonzeros).
-  medium-sample  the dataset record above as the line itself.
+The line (default, --workload dataset) measures BASELINE.json's metric on its own workload, "synthetic medium
+dataset, CSR SpMM K=32 fp64":
+  value     every --dataset-stride-th line of synthetic_matrices_medium_dataset (stride 80 = 203 matrices, K=32
+            fp64).  One STEP = one SpMM over every matrix of the sample: per matrix --warmup untimed launches, then
+            --steps launches timed by HIP events on the launch stream (a calibrated GPU-side pre-roll keeps host
+            enqueue gaps out of the timed region).  ms_per_step = the sum over matrices of the per-launch time;
+            value = sum(2*nnz*K) / ms_per_step = the aggregate GFLOP/s; roofline = sum of algorithmic bytes over the
+            same time, with the median / p10 / p90 per-matrix fractions, per-matrix PMC traffic when profiles/ holds
+            it for this engine build and the gather ceiling; cpu_baseline = the oracle's compute_csr on
+            a time-bounded subset of the same matrices (same A and B), whose C also checks the GPU's C bit for bit on
+            the rows the engine reports exact.
+            At N > 1 (weak scaling: the metric's workload sharded as independent matrices, no collective in the
+            data path) rank r runs its own stride-80 sample at offset r*80/N, so every GPU carries a statistically
+            equal share; value = the flops of all ranks / the max over ranks of their summed HIP-event time.
+  config2   (sub-record, N=1) BASELINE configs[1], SURVEY.md §8d: generator line
+            1000000 1000000 20 6.6667 normal random 0.3 100 0.95 0.5 14, K=32 fp64; --steps / --warmup launches, its
+            own roofline (PMC traffic, gather ceiling), CPU baseline with the oracle check over every row, and the
+            plugin end-to-end (PCIe) call.  At N > 1: config 2 weak (every rank a config-2-sized nnz-balanced row range
+            of one N-times-larger matrix), plus the in-process multi-GPU handle record.
+  config4   (sub-record, N > 1) BASELINE configs[3]: the largest avg-20 skew-10^4 line of
+            synthetic_matrices_large_dataset.txt with gamma row lengths (7477550 rows, 150 M nonzeros) split N ways
+            with the reference partitioner (strong scaling), B broadcast over RCCL once, max-over-ranks HIP-event
+            time, imbalance, C all-gathered once (timed).
+Other workloads (as the line itself):
+  config2   (N >= 1) the config-2 record above (--scaling strong: the single config-2 matrix split N ways).
+  config4   (N >= 1) the config-4 record above.
+  medium-sample  the dataset record with --dataset-iters / --dataset-warmup launches per matrix.
   twins     (config 5) the 52 validation twins (reference config.sh:283-339) at K=32, fp64 AND fp32: per dtype
             aggregate GFLOP/s and median fraction, and a cpu_baseline on every twin in the same run (time-bounded).
   pipeline   the sparse-attention pipeline consumer, fp32, n=512 (see run_pipeline).
@@ -86,8 +95,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
-    ap.add_argument("--workload", choices=["config2", "config4", "medium-sample", "twins", "pipeline"],
-                    default="config2")
+    ap.add_argument("--workload", choices=["dataset", "config2", "config4", "medium-sample", "twins", "pipeline"],
+                    default="dataset")
     ap.add_argument("--pipe-m", type=int, default=512, help="pipeline: weight rows = mask size")
     ap.add_argument("--pipe-k", type=int, default=512, help="pipeline: weight columns (rows of x)")
     ap.add_argument("--pipe-n", type=int, default=512, help="pipeline: columns of x (NUM_COLS)")
@@ -102,8 +111,14 @@ def parse():
     ap.add_argument("--dump-c", default=None, help="rank 0 writes a row sample of the (gathered) C + exact mask (npz)")
     ap.add_argument("--no-multi-handle", action="store_true",
                     help="N>1: skip the in-process multi-GPU handle record (peer vs RCCL B broadcast)")
-    ap.add_argument("--no-dataset", action="store_true", help="skip the medium-dataset sub-record (N=1)")
-    ap.add_argument("--dataset-stride", type=int, default=160, help="dataset: every n-th medium-dataset line")
+    ap.add_argument("--no-dataset", action="store_true",
+                    help="--workload dataset: skip the dataset pass (sub-records only; tests and PMC tools)")
+    ap.add_argument("--no-config2", action="store_true", help="--workload dataset: skip the config-2 sub-record")
+    ap.add_argument("--no-config4", action="store_true", help="--workload dataset, N > 1: skip the config-4 sub-record")
+    ap.add_argument("--strong-gen", default=None,
+                    help="override the config-4 generator line (the strong-split sub-record; tests use a small one)")
+    ap.add_argument("--dump-c-strong", default=None, help="rank 0 writes a row sample of the config-4 record's C (npz)")
+    ap.add_argument("--dataset-stride", type=int, default=80, help="dataset: every n-th medium-dataset line")
     ap.add_argument("--dataset-offset", type=int, default=0)
     ap.add_argument("--dataset-iters", type=int, default=10, help="dataset / twins: timed launches per matrix")
     ap.add_argument("--dataset-warmup", type=int, default=3)
@@ -186,19 +201,66 @@ def gather_rate_tbs(table_bytes: float) -> float:
     return pts[-1][1]
 
 
-def achievable(t_ms: float, traffic: float | None, l2_req: float | None, b_bytes: float) -> dict | None:
+def achievable(t_ms: float, traffic: float | None, l2_req: float | None, b_bytes: float,
+               bytes_alg: float | None = None) -> dict | None:
     """The gather ceiling of a launch: its measured past-L2 bytes at the chip's random-row gather rate
-    for a table of B's size, and its L2 requests (x 128 B) at the L2-resident gather rate; the larger time is the
-    ceiling.  frac_of_achievable = ceiling / measured (1.0 = at the ceiling)."""
+    for a table of B's size, its L2 requests (x 128 B) at the L2-resident gather rate, and (round 6) its compulsory
+    algorithmic bytes at the HBM peak; the largest time is the ceiling.  The third term matters where the gather
+    terms price streamed bytes at an on-chip rate: at K = 1 the past-L2 bytes are A's once-read stream (1.04x the
+    algorithmic bytes), which no launch moves faster than HBM, so without it the "ceiling" sat below the roofline
+    time itself.  frac_of_achievable = ceiling / measured (1.0 = at the ceiling)."""
     if traffic is None or t_ms <= 0:
         return None
     r = gather_rate_tbs(b_bytes)
     t_past = traffic / (r * 1e12) * 1e3
     t_l2 = (l2_req * L2_LINE) / (L2_GATHER_TBS * 1e12) * 1e3 if l2_req else 0.0
-    t = max(t_past, t_l2)
-    return {"t_ms": round(t, 5), "bound": "past-L2 gather" if t_past >= t_l2 else "L2 requests",
-            "past_l2_gather_tbs": round(r, 2), "t_past_l2_ms": round(t_past, 5), "t_l2_ms": round(t_l2, 5),
-            "frac_of_achievable": round(t / t_ms, 4)}
+    t_hbm = bytes_alg / (HBM_PEAK_GBS * 1e9) * 1e3 if bytes_alg else 0.0
+    t = max(t_past, t_l2, t_hbm)
+    bound = "HBM compulsory" if t == t_hbm and t_hbm > 0 else "past-L2 gather" if t_past >= t_l2 else "L2 requests"
+    return {"t_ms": round(t, 5), "bound": bound, "past_l2_gather_tbs": round(r, 2), "t_past_l2_ms": round(t_past, 5),
+            "t_l2_ms": round(t_l2, 5), "t_hbm_ms": round(t_hbm, 5), "frac_of_achievable": round(t / t_ms, 4)}
+
+
+_PREROLL: dict = {}
+
+
+def preroll(torch, stream, ms: float = 2.0) -> None:
+    """GPU-side pre-roll in front of a timed batch: a spin kernel of ~`ms` keeps the stream busy while the host
+    enqueues the timed launches, so a host-side stall (the generator thread, the garbage collector) never becomes an
+    idle gap between the events.  The events bracket only the launches; the spin rate is calibrated once."""
+    try:
+        if "cyc_per_ms" not in _PREROLL:
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(100_000)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                torch.cuda._sleep(2_000_000)
+                e1.record(stream)
+            torch.cuda.synchronize()
+            _PREROLL["cyc_per_ms"] = 2_000_000 / max(e0.elapsed_time(e1), 1e-3)
+        if _PREROLL["cyc_per_ms"]:
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(int(ms * _PREROLL["cyc_per_ms"]))
+    except Exception:  # no spin kernel in this torch build: time without a pre-roll
+        _PREROLL["cyc_per_ms"] = None
+
+
+def timed_launches(torch, stream, launch, iters: int) -> float:
+    """HIP-event time (ms) per launch of `iters` back-to-back launches on `stream`, behind a pre-roll."""
+    import gc
+    gc.collect()
+    gc.disable()
+    try:
+        preroll(torch, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(iters):
+            launch()
+        e1.record(stream)
+    finally:
+        gc.enable()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / max(iters, 1)
 
 
 def cpu_baseline(A, x_col, k: int, warmup: int, budget_s: float, dtype):
@@ -359,7 +421,8 @@ def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, 
     sample order while `cpu_budget_s` lasts (and `cpu_each_s` per matrix when set: twins).  Matrix generation runs
     one line ahead on a host thread (the generator releases the GIL), so the GPU does not wait for it."""
     from concurrent.futures import ThreadPoolExecutor
-    dev = torch.device("cuda", 0)
+    dev_index = torch.cuda.current_device()          # this rank's GPU (set by main before any record runs)
+    dev = torch.device("cuda", dev_index)
     tdt = torch.float64 if dtype == "f64" else torch.float32
     npdt = np.float64 if dtype == "f64" else np.float32
     dt_code = S.F64 if dtype == "f64" else S.F32
@@ -374,21 +437,17 @@ def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, 
     for i, line in enumerate(lines):
         A = fut.result()
         fut = ex.submit(lambda l: S.generate(S.gen_params(l)), lines[i + 1]) if i + 1 < len(lines) else None
-        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdt), A.m, A.ncols, A.nnz, K, 0)
+        mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdt), A.m, A.ncols, A.nnz, K, dev_index)
         g = torch.Generator(device=dev)
         g.manual_seed(42)
         B = torch.rand((max(A.ncols, 1), K), generator=g, device=dev, dtype=tdt)
         C = torch.empty((max(A.m, 1), K), device=dev, dtype=tdt)
+        def launch():
+            mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, stream.cuda_stream)
         for _ in range(warmup):
-            mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, stream.cuda_stream)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            launch()
         torch.cuda.synchronize()
-        ev0.record(stream)
-        for _ in range(iters):
-            mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, stream.cuda_stream)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        t = ev0.elapsed_time(ev1) / iters * 1e-3
+        t = timed_launches(torch, stream, launch, iters) * 1e-3
         chk = selfcheck(A, lambda cols: B[torch.from_numpy(cols).to(dev)].cpu().numpy(), C, K, npdt, nsample=32)
         bad += 0 if chk["ok"] else 1
         b = S.bytes_alg(A.m, A.ncols, A.nnz, K, dt_code)
@@ -400,7 +459,8 @@ def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, 
         pm = pmc.get(line)
         if pm and pm.get("nnz") == A.nnz:
             rec["traffic"] = pm["traffic_bytes"]
-            ach = achievable(t * 1e3, pm["traffic_bytes"], pm.get("tcc_req"), float(A.ncols) * K * (8 if dtype == "f64" else 4))
+            ach = achievable(t * 1e3, pm["traffic_bytes"], pm.get("tcc_req"), float(A.ncols) * K * (8 if dtype == "f64" else 4),
+                             b)
             rec["frac_of_achievable"] = ach["frac_of_achievable"] if ach else None
         if (cpu_left > 0 or cpu_each_s > 0) and A.nnz > 0:
             t0 = time.perf_counter()
@@ -476,17 +536,26 @@ def summarize(res: dict, K: int) -> dict:
     return out
 
 
-def run_dataset_record(args, torch, S, np) -> dict:
+def run_dataset_record(args, torch, S, np, iters: int | None = None, warmup: int | None = None, offset: int | None = None,
+                       cpu: bool = True, pmc_on: bool = True) -> dict:
+    """The metric's own workload: every stride-th medium-dataset line from `offset`, `iters` timed launches each."""
     from spmm_amd.datasets import medium_dataset_lines
-    lines = medium_dataset_lines()[args.dataset_offset::args.dataset_stride]
-    pmc = load_pmc_dataset(args.pmc_dataset, args.k, args.dtype)
-    res = run_lines(lines, args.k, args.dtype, args.dataset_iters, args.dataset_warmup, torch, S, np,
-                    cpu_budget_s=0.0 if args.no_cpu_baseline else args.dataset_cpu_seconds, pmc=pmc)
+    iters = args.dataset_iters if iters is None else iters
+    warmup = args.dataset_warmup if warmup is None else warmup
+    offset = args.dataset_offset if offset is None else offset
+    lines = medium_dataset_lines()[offset::args.dataset_stride]
+    pmc = load_pmc_dataset(args.pmc_dataset, args.k, args.dtype) if pmc_on else {}
+    res = run_lines(lines, args.k, args.dtype, iters, warmup, torch, S, np,
+                    cpu_budget_s=0.0 if (args.no_cpu_baseline or not cpu) else args.dataset_cpu_seconds, pmc=pmc)
     rec = summarize(res, args.k)
     rec.update({"metric": METRIC, "scaling": "single-gpu", "dtype": args.dtype,
                 "workload": f"every {args.dataset_stride}th line of synthetic_matrices_medium_dataset from "
-                            f"{args.dataset_offset} ({len(lines)} matrices), K={args.k}",
-                "iters_per_matrix": args.dataset_iters, "warmup_per_matrix": args.dataset_warmup})
+                            f"{offset} ({len(lines)} matrices), K={args.k}",
+                "iters_per_matrix": iters, "warmup_per_matrix": warmup,
+                "ms_per_pass": round(sum(r["ms"] for r in res["recs"]), 5),
+                "flops_per_pass": sum(r["flops"] for r in res["recs"]),
+                "bytes_alg_per_pass": sum(r["bytes_alg"] for r in res["recs"]),
+                "nnz_total": int(sum(r["nnz"] for r in res["recs"]))})
     return rec
 
 
@@ -701,6 +770,316 @@ def dump_c(path: str, C_all, exact_all, k: int) -> None:
     np.savez(path, rows=rows, c=c, exact=np.asarray(exact_all)[rows], k=np.int64(k))
 
 
+class Ctx:
+    """Per-process run context: world, rank, process group, device, and the imported modules."""
+
+    def __init__(self, args, N, rank, dist, dev, dev_index, torch, S, np, sharding):
+        self.args, self.N, self.rank, self.dist = args, N, rank, dist
+        self.dev, self.dev_index, self.torch, self.S, self.np, self.sharding = dev, dev_index, torch, S, np, sharding
+
+    def barrier(self):
+        self.torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+
+def measure_line(ctx: Ctx, gen: str, scaling: str, workload: str, cpu: bool, e2e: bool, multi: bool,
+                 dump: str | None) -> tuple[dict, bool]:
+    """One generator line as one SpMM per step: the global matrix (scaling "weak": the line's shape N times over;
+    "strong": the line itself) split into N nnz-balanced row ranges with the reference partitioner, this rank's rows
+    generated and planned, B drand48(42) broadcast once, --warmup untimed and --steps timed launches bracketed by a
+    barrier + synchronize on both sides, value from the max over ranks of the HIP-event time.  Returns (record, ok)
+    on every rank (the record is complete on rank 0)."""
+    args, N, rank, dist, dev, torch, S, np = ctx.args, ctx.N, ctx.rank, ctx.dist, ctx.dev, ctx.torch, ctx.S, ctx.np
+    sharding = ctx.sharding
+    K = args.k
+    tdtype = torch.float64 if args.dtype == "f64" else torch.float32
+    npdtype = np.float64 if args.dtype == "f64" else np.float32
+
+    # ---- this rank's shard of the global matrix (nnz-balanced row split, a8 partitioner)
+    t0 = time.perf_counter()
+    p = sharding.weak_scaled_params(gen, N) if (N > 1 and scaling == "weak") else S.gen_params(gen)
+    rp_global = S.generate_row_ptr(p)
+    nnz_total = int(rp_global[-1])
+    bounds = [S.partition_rows(rp_global, nnz_total, N, w) for w in range(N)]
+    r0, r1 = bounds[rank]
+    A = S.generate_rows(p, r0, r1) if N > 1 else S.generate(p)
+    per_rank = [int(rp_global[e] - rp_global[s]) for s, e in bounds]
+    imbalance = max(per_rank) / (sum(per_rank) / N) if nnz_total else 1.0
+    del rp_global
+    t_gen = time.perf_counter() - t0
+    ncols = int(p.nr_cols)
+
+    t0 = time.perf_counter()
+    mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdtype), A.m, ncols, A.nnz, K, ctx.dev_index)
+    t_plan = time.perf_counter() - t0
+
+    # ---- B: drand48(42) column-major x on rank 0 (the reference harness convention), row-major in HBM, broadcast
+    x_col = Bh = None
+    if rank == 0:
+        x_col = S.drand48(42, ncols * K)
+        Bh = np.ascontiguousarray(x_col.reshape(K, ncols).T).astype(npdtype)
+        B = torch.from_numpy(Bh).to(dev)
+    else:
+        B = torch.empty((ncols, K), device=dev, dtype=tdtype)
+    t_bcast = 0.0
+    if dist is not None:
+        ctx.barrier()
+        tb = time.perf_counter()
+        sharding.broadcast_b(dist, B)        # RCCL over xGMI, once at setup
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - tb
+    C = torch.empty((max(A.m, 1), K), device=dev, dtype=tdtype)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step():
+        mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, sptr)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    kern_ms = timed_launches(torch, stream, step, args.steps)      # HIP events on the launch stream, per step
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0                             # barrier-inclusive wall time of the K steps
+    bytes_launch = S.bytes_alg(A.m, ncols, A.nnz, K, S.F64 if args.dtype == "f64" else S.F32)
+    kern_all, bytes_all = [kern_ms], [bytes_launch]
+    if dist is not None:
+        kt = sharding.gather_scalars(dist, [kern_ms, bytes_launch, elapsed], dev)
+        kern_all = [v[0] for v in kt]
+        bytes_all = [v[1] for v in kt]
+        elapsed = max(v[2] for v in kt)
+    slow = int(np.argmax(kern_all))
+    kern_max_ms = kern_all[slow]
+
+    # ---- C all-gather, once, timed (validation / hand-back path, never inside the timed loop)
+    t_gather = None
+    exact = mf.exact_rows()
+    c_all, exact_all = C[: A.m], exact
+    if dist is not None:
+        counts = [e - s for s, e in bounds]
+        ctx.barrier()
+        tg = time.perf_counter()
+        c_all = sharding.allgather_rows(dist, C[: max(A.m, 1)], counts)
+        torch.cuda.synchronize()
+        t_gather = time.perf_counter() - tg
+        ex_t = torch.from_numpy(exact.astype(np.uint8).reshape(-1, 1)).to(dev)
+        exact_all = sharding.allgather_rows(dist, ex_t if A.m else torch.zeros((1, 1), dtype=torch.uint8, device=dev),
+                                            counts).cpu().numpy().ravel().astype(bool)
+    if rank == 0 and dump:
+        dump_c(dump, c_all, exact_all, K)
+    del c_all
+
+    # ---- self-check on every rank (B rows for the check: rank 0 has them on the host; others copy from HBM)
+    Bh_chk = Bh if rank == 0 else B.cpu().numpy()
+    chk = selfcheck(A, Bh_chk, C, K, npdtype)
+    ok_all = chk["ok"]
+    if dist is not None:
+        ok_all = all(v[0] == 0 for v in sharding.gather_scalars(dist, [0.0 if chk["ok"] else 1.0], dev))
+
+    flops_step = 2.0 * nnz_total * K
+    gflops = flops_step / (kern_max_ms * 1e-3) / 1e9
+    # the slowest rank bounds the step: its bytes over its time (one definition at every N: the rank's rows and
+    # nonzeros with the global column count)
+    achieved = bytes_all[slow] / (kern_max_ms * 1e-3) / 1e9
+    traffic = l2_req = None
+    try:
+        pm = json.loads(Path(args.pmc_json).read_text())
+        if (pm.get("workload") == gen and pm.get("k") == K and pm.get("dtype") == args.dtype and N == 1
+                and pm.get("nnz") == A.nnz and pm.get("engine_sha256") == engine_sha256()):
+            traffic = pm.get("hbm_bytes_per_launch")
+            cc = pm.get("counters_per_launch", {})
+            if "TCC_HIT_sum" in cc and "TCC_MISS_sum" in cc:
+                l2_req = cc["TCC_HIT_sum"] + cc["TCC_MISS_sum"]
+    except Exception:
+        pass
+    ach = achievable(kern_max_ms, traffic, l2_req, float(ncols) * K * (8 if args.dtype == "f64" else 4),
+                     bytes_all[slow])
+
+    # ---- plugin end to end (N=1): host x / y through the reference contract (H2D + transpose + kernel + D2H)
+    e2e_rec = None
+    if N == 1 and e2e:
+        y = np.empty(A.m * K, npdtype)
+        xh = x_col.astype(npdtype)
+        mf.spmm(xh, y, K)
+        te = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            mf.spmm(xh, y, K)
+            te.append(time.perf_counter() - t1)
+        lt = mf.last_times()
+        e2e_rec = {"ms_per_call": round(sorted(te)[1] * 1e3, 3),
+                   "gflops": round(flops_step / sorted(te)[1] / 1e9, 2),
+                   "events_ms": {k_: round(v, 4) for k_, v in lt.items()},
+                   "note": "pageable host buffers; PCIe-inclusive, never the headline value"}
+        del y, xh
+
+    cpu_rec = None
+    if rank == 0 and N == 1 and cpu and not args.no_cpu_baseline:
+        want = None
+        try:
+            want, cpu_rec = cpu_baseline(A, x_col, K, args.cpu_warmup, args.cpu_seconds, npdtype)
+        except Exception as e:  # the baseline is reported, never required
+            cpu_rec = {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
+        if want is not None:
+            # the baseline's own C checks this run's C over every row (bit-exact where the engine reports exact); a
+            # failure of the check itself fails the record, it is never reported as a baseline failure (ADVICE r05)
+            try:
+                cpu_rec["oracle_check"] = oracle_compare(A, x_col, K, C[: A.m].cpu().numpy(), want, exact, npdtype)
+            except Exception as e:
+                cpu_rec["oracle_check"] = {"ok": False, "error": f"{type(e).__name__}: {e}"}
+            ok_all = ok_all and cpu_rec["oracle_check"]["ok"]
+            del want
+    mf.close()
+    del C
+
+    # ---- N>1: the in-process multi-GPU handle of the C ABI over the same matrix (rank 0; the others wait)
+    multi_rec = None
+    if dist is not None and multi and not args.no_multi_handle:
+        if rank == 0:
+            devs = [0] * N if args.dist_backend == "gloo" else list(range(N))
+            try:
+                multi_rec = run_multi_handle(args, torch, S, np, p, K, npdtype, B, Bh, devs, stream)
+            except Exception as e:   # reported, the distributed record stands on its own
+                multi_rec = {"error": f"{type(e).__name__}: {e}"}
+        dist.barrier()
+    del B
+
+    rec = {
+        "metric": METRIC,
+        "value": round(gflops, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(kern_max_ms, 5),
+        "higher_is_better": True,
+        "scaling": scaling if N > 1 else "single-gpu",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (own generator, seeded; A values U[0.5,1.5), B drand48(42))",
+        "config": {"workload": f"{workload}: csr_spmm gen='{gen}'"
+                               + (f" x{N} stacked (weak)" if scaling == "weak" and N > 1 else "")
+                               + f", K={K}",
+                   "nnz_total": nnz_total, "rows_total": int(p.nr_rows), "cols": ncols, "k": K,
+                   "nnz_per_rank": per_rank, "imbalance_max_over_mean": round(imbalance, 4),
+                   "parallelism": f"row-shard{N}" if N > 1 else "single-gpu",
+                   "dist_backend": args.dist_backend if N > 1 else None},
+        "timing": "value = 2*nnz*K / (max over ranks of the HIP-event time per step of the K timed steps, launch "
+                  "stream); wall_ms_per_step = barrier-inclusive host wall time, max over ranks",
+        "wall_ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 5),
+        "hbm_gbs_alg": round(achieved, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_gbs": None if traffic is None else round(traffic / (kern_max_ms * 1e-3) / 1e9, 1),
+                     "achievable": ach,
+                     "bytes_alg_per_launch": bytes_all[slow], "kernel_ms_per_launch": round(kern_max_ms, 5),
+                     "kernel_ms_per_rank": [round(v, 5) for v in kern_all], "slowest_rank": slow},
+        "cpu_baseline": cpu_rec,
+        "plugin_e2e": e2e_rec,
+        "multi_handle": multi_rec,
+        "setup": {"gen_s": round(t_gen, 2), "plan_s": round(t_plan, 2), "bcast_B_s": round(t_bcast, 4),
+                  "bcast_B_s_modes": None if multi_rec is None or "modes" not in multi_rec else
+                  {"torch.distributed rccl (one process per GPU)": round(t_bcast, 4),
+                   **{f"multi-handle {m_}": v_.get("bcast_B_s") for m_, v_ in multi_rec["modes"].items()}},
+                  "allgather_C_s": None if t_gather is None else round(t_gather, 4),
+                  "selfcheck": chk, "selfcheck_all_ranks_ok": ok_all},
+    }
+    return rec, ok_all
+
+
+def run_dataset_line(ctx: Ctx) -> tuple[dict, bool]:
+    """The default line: the medium-dataset sample as the value (every rank its own stride sample at N > 1), with
+    the config-2 record (N = 1) or the config-4 strong split and the config-2 weak record (N > 1) beside it."""
+    args, N, rank, torch, S, np = ctx.args, ctx.N, ctx.rank, ctx.torch, ctx.S, ctx.np
+    from spmm_amd.datasets import CONFIG2_LINE, CONFIG4_LINE
+    ok = True
+    sub = {}
+    # ---- sub-records first (they allocate and free whole-GPU buffers; the dataset pass then runs on a clean heap)
+    if N == 1 and not args.no_config2:
+        rec, ok2 = measure_line(ctx, CONFIG2_LINE, "strong", "config2", cpu=True, e2e=True, multi=False,
+                                dump=args.dump_c)
+        sub["config2"] = rec
+        ok = ok and ok2
+    if N > 1 and not args.no_config4:
+        rec, ok4 = measure_line(ctx, args.strong_gen or CONFIG4_LINE, "strong", "config4", cpu=False, e2e=False,
+                                multi=False, dump=args.dump_c_strong)
+        sub["config4_strong"] = rec
+        ok = ok and ok4
+    if N > 1 and not args.no_config2:
+        rec, ok2 = measure_line(ctx, CONFIG2_LINE, "weak", "config2", cpu=False, e2e=False, multi=True,
+                                dump=args.dump_c)
+        sub["config2_weak"] = rec
+        ok = ok and ok2
+
+    # ---- the dataset pass (one step = every matrix of the rank's sample once)
+    ds = None
+    if not args.no_dataset:
+        offset = args.dataset_offset + (rank * args.dataset_stride) // N
+        ctx.barrier()
+        t0 = time.perf_counter()
+        ds = run_dataset_record(args, torch, S, np, iters=args.steps, warmup=args.warmup, offset=offset,
+                                cpu=(rank == 0 and N == 1), pmc_on=(N == 1))
+        wall = time.perf_counter() - t0
+        ctx.barrier()
+        mine = [ds["ms_per_pass"], ds["flops_per_pass"], ds["bytes_alg_per_pass"], float(ds["matrices"]),
+                float(ds["selfcheck_failures"]), wall]
+        allr = ctx.sharding.gather_scalars(ctx.dist, mine, ctx.dev) if ctx.dist is not None else [mine]
+        ds["selfcheck_failures_all_ranks"] = int(sum(v[4] for v in allr))
+        ok = ok and ds["selfcheck_failures_all_ranks"] == 0
+        ms = [v[0] for v in allr]
+        slow = int(np.argmax(ms))
+        flops = sum(v[1] for v in allr)
+        ds["ranks"] = [{"ms_per_pass": round(v[0], 5), "gflops": round(v[1] / (v[0] * 1e-3) / 1e9, 3),
+                        "matrices": int(v[3]), "wall_s": round(v[5], 1)} for v in allr]
+        ds["value_all_ranks"] = round(flops / (ms[slow] * 1e-3) / 1e9, 3)
+        ds["ms_per_step_max_over_ranks"] = round(ms[slow], 5)
+        ds["slowest_rank"] = slow
+    if rank != 0:
+        return {}, ok
+
+    if ds is None:   # sub-records only (tests, PMC tools): the first one is the line
+        key = next(iter(sub))
+        line = dict(sub.pop(key))
+        line["sub_records"] = sub
+        return line, ok
+    data_desc = "synthetic (own generator, seeded; A values U[0.5,1.5), B torch.rand(seed 42) per matrix)"
+    n_mat = sum(r["matrices"] for r in ds["ranks"])
+    line = {
+        "metric": METRIC,
+        "value": ds["value_all_ranks"],
+        "unit": "GFLOP/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ds["ms_per_step_max_over_ranks"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": data_desc,
+        "config": {"workload": (f"synthetic_matrices_medium_dataset, every {args.dataset_stride}th line"
+                                + (f" from {args.dataset_offset}" if N == 1 else
+                                   f", rank r from offset {args.dataset_offset} + r*{args.dataset_stride}/{N}")
+                                + f" ({n_mat} matrices), CSR SpMM K={args.k} {args.dtype}"),
+                   "matrices": n_mat, "matrices_per_rank": [r["matrices"] for r in ds["ranks"]],
+                   "k": args.k, "parallelism": f"matrix-shard{N}" if N > 1 else "single-gpu",
+                   "dist_backend": args.dist_backend if N > 1 else None},
+        "timing": ("one step = one SpMM over every matrix of the rank's sample; per matrix --warmup untimed and "
+                   "--steps HIP-event-timed launches on the launch stream (behind a GPU pre-roll); ms_per_step = sum "
+                   "over matrices of the per-launch time, max over ranks; value = flops of all ranks / ms_per_step"),
+        "roofline": ds["roofline"],
+        "cpu_baseline": ds["cpu_baseline"],
+        "oracle_check": ds.get("oracle_check"),
+        "dataset": {k_: v_ for k_, v_ in ds.items() if k_ not in ("roofline", "cpu_baseline", "oracle_check")},
+        **sub,
+        "setup": {"selfcheck_failures_all_ranks": ds["selfcheck_failures_all_ranks"], "all_ok": ok},
+    }
+    return line, ok
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -747,224 +1126,21 @@ def main():
             dist.init_process_group(backend="nccl", device_id=dev)
         else:
             dist.init_process_group(backend="gloo")
-    K = args.k
-    tdtype = torch.float64 if args.dtype == "f64" else torch.float32
-    npdtype = np.float64 if args.dtype == "f64" else np.float32
-    gen = args.gen or (CONFIG4_LINE if args.workload == "config4" else CONFIG2_LINE)
-    scaling = args.scaling
+    ctx = Ctx(args, N, rank, dist, dev, dev_index, torch, S, np, sharding)
 
-    # ---- this rank's shard of the global matrix (nnz-balanced row split, a8 partitioner)
-    t0 = time.perf_counter()
-    p = sharding.weak_scaled_params(gen, N) if (N > 1 and scaling == "weak") else S.gen_params(gen)
-    rp_global = S.generate_row_ptr(p)
-    nnz_total = int(rp_global[-1])
-    bounds = [S.partition_rows(rp_global, nnz_total, N, w) for w in range(N)]
-    r0, r1 = bounds[rank]
-    A = S.generate_rows(p, r0, r1) if N > 1 else S.generate(p)
-    per_rank = [int(rp_global[e] - rp_global[s]) for s, e in bounds]
-    imbalance = max(per_rank) / (sum(per_rank) / N) if nnz_total else 1.0
-    del rp_global
-    t_gen = time.perf_counter() - t0
-    ncols = int(p.nr_cols)
-
-    t0 = time.perf_counter()
-    mf = S.csr_to_format(A.row_ptr, A.col_idx, A.values.astype(npdtype), A.m, ncols, A.nnz, K, dev_index)
-    t_plan = time.perf_counter() - t0
-
-    # ---- B: drand48(42) column-major x on rank 0 (the reference harness convention), row-major in HBM, broadcast
-    x_col = None
-    if rank == 0:
-        x_col = S.drand48(42, ncols * K)
-        Bh = np.ascontiguousarray(x_col.reshape(K, ncols).T).astype(npdtype)
-        B = torch.from_numpy(Bh).to(dev)
+    if args.workload == "dataset":
+        line, ok_all = run_dataset_line(ctx)
     else:
-        B = torch.empty((ncols, K), device=dev, dtype=tdtype)
-    t_bcast = 0.0
-    if dist is not None:
-        torch.cuda.synchronize()
-        dist.barrier()
-        tb = time.perf_counter()
-        sharding.broadcast_b(dist, B)        # RCCL over xGMI, once at setup
-        torch.cuda.synchronize()
-        t_bcast = time.perf_counter() - tb
-    C = torch.empty((max(A.m, 1), K), device=dev, dtype=tdtype)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
-
-    def step():
-        mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, C.data_ptr(), K, sptr)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0                       # barrier-inclusive wall time of the K steps
-    kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)     # HIP events on the launch stream, per step
-    bytes_launch = S.bytes_alg(A.m, ncols, A.nnz, K, S.F64 if args.dtype == "f64" else S.F32)
-    kern_all, bytes_all = [kern_ms], [bytes_launch]
-    if dist is not None:
-        kt = sharding.gather_scalars(dist, [kern_ms, bytes_launch, elapsed], dev)
-        kern_all = [v[0] for v in kt]
-        bytes_all = [v[1] for v in kt]
-        elapsed = max(v[2] for v in kt)
-    slow = int(np.argmax(kern_all))
-    kern_max_ms = kern_all[slow]
-
-    # ---- C all-gather, once, timed (validation / hand-back path, never inside the timed loop)
-    t_gather = None
-    exact = mf.exact_rows()
-    c_all, exact_all = C[: A.m], exact
-    if dist is not None:
-        counts = [e - s for s, e in bounds]
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter()
-        c_all = sharding.allgather_rows(dist, C[: max(A.m, 1)], counts)
-        torch.cuda.synchronize()
-        t_gather = time.perf_counter() - tg
-        ex_t = torch.from_numpy(exact.astype(np.uint8).reshape(-1, 1)).to(dev)
-        exact_all = sharding.allgather_rows(dist, ex_t if A.m else torch.zeros((1, 1), dtype=torch.uint8, device=dev),
-                                            counts).cpu().numpy().ravel().astype(bool)
-    if rank == 0 and args.dump_c:
-        dump_c(args.dump_c, c_all, exact_all, K)
-    del c_all
-
-    # ---- self-check on every rank (B rows for the check: rank 0 has them on the host; others copy from HBM)
-    Bh_chk = Bh if rank == 0 else B.cpu().numpy()
-    chk = selfcheck(A, Bh_chk, C, K, npdtype)
-    ok_local = chk["ok"]
-    if dist is not None:
-        ok_all = all(v[0] == 0 for v in sharding.gather_scalars(dist, [0.0 if ok_local else 1.0], dev))
-    else:
-        ok_all = ok_local
-
-    flops_step = 2.0 * nnz_total * K
-    gflops = flops_step / (kern_max_ms * 1e-3) / 1e9
-    # the slowest rank bounds the step: its bytes over its time (one definition at every N: the rank's rows and
-    # nonzeros with the global column count)
-    achieved = bytes_all[slow] / (kern_max_ms * 1e-3) / 1e9
-    traffic = l2_req = None
-    try:
-        pm = json.loads(Path(args.pmc_json).read_text())
-        if (pm.get("workload") == gen and pm.get("k") == K and pm.get("dtype") == args.dtype and N == 1
-                and pm.get("nnz") == A.nnz and pm.get("engine_sha256") == engine_sha256()):
-            traffic = pm.get("hbm_bytes_per_launch")
-            cc = pm.get("counters_per_launch", {})
-            if "TCC_HIT_sum" in cc and "TCC_MISS_sum" in cc:
-                l2_req = cc["TCC_HIT_sum"] + cc["TCC_MISS_sum"]
-    except Exception:
-        pass
-    ach = achievable(kern_max_ms, traffic, l2_req, float(ncols) * K * (8 if args.dtype == "f64" else 4))
-
-    # ---- plugin end to end (N=1): host x / y through the reference contract (H2D + transpose + kernel + D2H)
-    e2e = None
-    if N == 1 and args.workload == "config2":
-        y = np.empty(A.m * K, npdtype)
-        xh = x_col.astype(npdtype)
-        mf.spmm(xh, y, K)
-        te = []
-        for _ in range(3):
-            t1 = time.perf_counter()
-            mf.spmm(xh, y, K)
-            te.append(time.perf_counter() - t1)
-        lt = mf.last_times()
-        e2e = {"ms_per_call": round(sorted(te)[1] * 1e3, 3),
-               "gflops": round(flops_step / sorted(te)[1] / 1e9, 2),
-               "events_ms": {k_: round(v, 4) for k_, v in lt.items()},
-               "note": "pageable host buffers; PCIe-inclusive, never the headline value"}
-        del y, xh
-
-    cpu = None
-    if rank == 0 and N == 1 and args.workload == "config2" and not args.no_cpu_baseline:
-        try:
-            want, cpu = cpu_baseline(A, x_col, K, args.cpu_warmup, args.cpu_seconds, npdtype)
-            # the baseline's own C checks this run's C over every row (bit-exact where the engine reports exact)
-            cpu["oracle_check"] = oracle_compare(A, x_col, K, C[: A.m].cpu().numpy(), want, exact, npdtype)
-            ok_all = ok_all and cpu["oracle_check"]["ok"]
-            del want
-        except Exception as e:  # the baseline is reported, never required
-            cpu = {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
-    mf.close()
-    del C
-
-    # ---- N>1: the in-process multi-GPU handle of the C ABI over the same matrix (rank 0; the others wait)
-    multi = None
-    if dist is not None and not args.no_multi_handle:
-        if rank == 0:
-            devs = [0] * N if args.dist_backend == "gloo" else list(range(N))
-            try:
-                multi = run_multi_handle(args, torch, S, np, p, K, npdtype, B, Bh, devs, stream)
-            except Exception as e:   # reported, the distributed line stands on its own
-                multi = {"error": f"{type(e).__name__}: {e}"}
-        dist.barrier()
-    del B
-
-    dataset = None
-    dataset_ok = True
-    if rank == 0 and N == 1 and args.workload == "config2" and not args.no_dataset and args.gen is None:
-        dataset = run_dataset_record(args, torch, S, np)
-        dataset_ok = dataset["selfcheck_failures"] == 0
-
+        gen = args.gen or (CONFIG4_LINE if args.workload == "config4" else CONFIG2_LINE)
+        line, ok_all = measure_line(ctx, gen, args.scaling, args.workload, cpu=(args.workload == "config2"),
+                                    e2e=(args.workload == "config2"), multi=True, dump=args.dump_c)
     if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(gflops, 3),
-            "unit": "GFLOP/s",
-            "n_gpus": N,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(kern_max_ms, 5),
-            "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": None,
-            "dtype": args.dtype,
-            "data": "synthetic (own generator, seeded; A values U[0.5,1.5), B drand48(42))",
-            "config": {"workload": f"{args.workload}: csr_spmm gen='{gen}'"
-                                   + (f" x{N} stacked (weak)" if scaling == "weak" and N > 1 else "")
-                                   + f", K={K}",
-                       "nnz_total": nnz_total, "rows_total": int(p.nr_rows), "cols": ncols, "k": K,
-                       "nnz_per_rank": per_rank, "imbalance_max_over_mean": round(imbalance, 4),
-                       "parallelism": f"row-shard{N}" if N > 1 else "single-gpu",
-                       "dist_backend": args.dist_backend if N > 1 else None},
-            "timing": "value = 2*nnz*K / (max over ranks of the HIP-event time per step of the K timed steps, launch "
-                      "stream); wall_ms_per_step = barrier-inclusive host wall time, max over ranks",
-            "wall_ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "hbm_gbs_alg": round(achieved, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_gbs": None if traffic is None else round(traffic / (kern_max_ms * 1e-3) / 1e9, 1),
-                         "achievable": ach,
-                         "bytes_alg_per_launch": bytes_all[slow], "kernel_ms_per_launch": round(kern_max_ms, 5),
-                         "kernel_ms_per_rank": [round(v, 5) for v in kern_all], "slowest_rank": slow},
-            "cpu_baseline": cpu,
-            "plugin_e2e": e2e,
-            "dataset": dataset,
-            "multi_handle": multi,
-            "setup": {"gen_s": round(t_gen, 2), "plan_s": round(t_plan, 2), "bcast_B_s": round(t_bcast, 4),
-                      "bcast_B_s_modes": None if multi is None or "modes" not in multi else
-                      {"torch.distributed rccl (one process per GPU)": round(t_bcast, 4),
-                       **{f"multi-handle {m_}": v_.get("bcast_B_s") for m_, v_ in multi["modes"].items()}},
-                      "allgather_C_s": None if t_gather is None else round(t_gather, 4),
-                      "selfcheck": chk, "selfcheck_all_ranks_ok": ok_all},
-        }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
-    if not ok_all or not dataset_ok:
-        print("error: self-check failed (C not finite or outside the normwise bound)", file=sys.stderr)
+    if not ok_all:
+        print("error: self-check failed (C not finite, outside the normwise bound, or not bit-exact against the "
+              "oracle on an exact row)", file=sys.stderr)
         sys.exit(1)
 
 

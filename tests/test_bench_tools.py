@@ -28,6 +28,19 @@ def test_achievable_takes_the_larger_bound():
     assert bench.achievable(1.0, None, None, 1e6) is None
 
 
+def test_achievable_never_below_the_hbm_roofline_time():
+    """K = 1, 72652 x 500 (round-5 PMC): 0.437 GB of compulsory bytes, past-L2 traffic 1.04x of them, B 0.6 MB.  The
+    gather terms price that stream at the L2-resident rate (a 0.024-ms "ceiling"); the HBM term keeps the ceiling at
+    or above the roofline time of the compulsory bytes."""
+    alg = 437.0e6
+    a = bench.achievable(0.1042, 1.04 * alg, 5.29e6, 72652 * 8, alg)
+    assert a["bound"] == "HBM compulsory"
+    assert a["t_ms"] == pytest.approx(alg / 8e12 * 1e3, rel=1e-3) and a["t_hbm_ms"] == a["t_ms"]
+    assert a["t_ms"] > max(a["t_past_l2_ms"], a["t_l2_ms"])
+    b = bench.achievable(0.41565, 3.131956852e9, 34.18e6, 1e6 * 32 * 8, 755999464.0)   # config 2: gather-bound
+    assert b["bound"] == "past-L2 gather" and b["t_hbm_ms"] < b["t_ms"]
+
+
 def test_pmc_dataset_records_are_keyed_by_engine_build(tmp_path):
     sha = bench.engine_sha256()
     recs = [{"gen": "a", "k": 32, "dtype": "f64", "engine_sha256": sha, "traffic_bytes": 1.0},

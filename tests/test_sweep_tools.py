@@ -132,39 +132,62 @@ def test_sweep_compare_speedups(tmp_path):
 
 def test_gpu_rwlock_writer_excludes_readers_and_is_not_starved(tmp_path):
     """tools/gpu_rwlock.py: readers share; a writer waits for the readers inside, and a reader arriving after the
-    writer waits for it (writer preference) -- checked with three processes and a shared event log."""
+    writer waits for it (writer preference) -- checked with three processes and a shared event log.  The arrival
+    order is forced by events, not delays: W starts once R1 is inside, R2 once W holds the gate, and R1
+    leaves only after R2 has started waiting."""
+    import errno
+    import fcntl
     import multiprocessing as mp
     import time
     from gpu_rwlock import GpuRWLock
     path, log = str(tmp_path / "gpu.lock"), tmp_path / "log.txt"
+    ctx = mp.get_context("fork")
+    r1_in, w_start, r2_wait = ctx.Event(), ctx.Event(), ctx.Event()
 
     def note(s):
         with open(log, "a") as f:
-            f.write(f"{time.monotonic():.4f} {s}\n")
+            f.write(f"{time.monotonic():.6f} {s}\n")
 
-    def reader(name, delay, hold):
-        time.sleep(delay)
+    def reader1():
         lk = GpuRWLock(path)
         with lk.shared():
-            note(f"{name} in")
-            time.sleep(hold)
-            note(f"{name} out")
+            note("R1 in")
+            r1_in.set()
+            assert r2_wait.wait(20)
+            time.sleep(0.2)               # R2 is blocked at the gate by now; the order below holds either way
+            note("R1 out")
 
-    def writer(delay, hold):
-        time.sleep(delay)
+    def writer():
+        assert r1_in.wait(20)
         lk = GpuRWLock(path)
+        w_start.set()
         with lk.exclusive():
             note("W in")
-            time.sleep(hold)
+            time.sleep(0.1)
             note("W out")
 
-    ctx = mp.get_context("fork")
-    ps = [ctx.Process(target=reader, args=("R1", 0.0, 0.6)), ctx.Process(target=writer, args=(0.2, 0.4)),
-          ctx.Process(target=reader, args=("R2", 0.4, 0.1))]
+    def reader2():
+        assert w_start.wait(20)
+        gate = open(path + ".gate", "a+")
+        while True:                        # wait until the writer holds the gate
+            try:
+                fcntl.flock(gate, fcntl.LOCK_EX | fcntl.LOCK_NB)
+                fcntl.flock(gate, fcntl.LOCK_UN)
+                time.sleep(0.01)
+            except OSError as e:
+                assert e.errno in (errno.EWOULDBLOCK, errno.EAGAIN)
+                break
+        lk = GpuRWLock(path)
+        r2_wait.set()
+        with lk.shared():
+            note("R2 in")
+            note("R2 out")
+
+    ps = [ctx.Process(target=reader1), ctx.Process(target=writer), ctx.Process(target=reader2)]
     for p in ps:
         p.start()
     for p in ps:
-        p.join(10)
+        p.join(60)
         assert p.exitcode == 0
     ev = [l.split(" ", 1)[1] for l in sorted(log.read_text().splitlines())]
     assert ev == ["R1 in", "R1 out", "W in", "W out", "R2 in", "R2 out"]

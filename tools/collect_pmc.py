@@ -66,7 +66,8 @@ def main():
     ap.add_argument("--no-latest", action="store_true",
                     help="do not overwrite profiles/pmc_latest.json (the bench line's traffic source, config 2 only)")
     args = ap.parse_args()
-    bench_args = ["--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--no-dataset", "--k", str(args.k)]
+    bench_args = ["--workload", "config2", "--steps", str(args.steps), "--warmup", "2", "--no-cpu-baseline", "--k",
+                  str(args.k)]
     if args.gen:
         bench_args += ["--gen", args.gen]
     outdir = ROOT / "gpurun_out" / "pmc"

@@ -14,10 +14,10 @@ write bytes = WRITE_SIZE KiB; both sit on the L2 memory side, so Infinity-Cache 
 an upper bound on true HBM bytes).  Rate = traffic / kernel time (the union of the engine kernels' intervals: the
 matrix-core plans overlap kernels on a side stream).  Each record carries the engine build's
 fingerprint (bench.engine_sha256), the L2 requests (TCC_HIT + TCC_MISS) and the gather-ceiling fraction
-(bench.achievable); bench.py reads these records for its dataset sub-record.
+(bench.achievable); bench.py reads these records for its dataset line.
 
 Sets:  --set stratified --per-class N   N lines of every (avg nnz/row, bw) class, evenly spaced in dataset order
-       --set sample --stride S          every S-th dataset line (bench.py's dataset sub-record: S = 160)
+       --set sample --stride S          every S-th dataset line (bench.py's dataset line: S = 80)
   python tools/pmc_dataset.py collect --set sample --stride 160 --out gpurun_out/pmc_dataset/sample160.jsonl
 """
 import argparse

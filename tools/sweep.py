@@ -10,9 +10,9 @@ the CPU oracle (bit-exact on the rows the engine reports exact, normwise 1e-10 o
 gpurun calls (tools/sweep_resumable.sh).  --budget bounds the wall time.
 
 The host side (generation, the inspector's plan per K, the oracle check) costs 10-50x the timed launches, so
---workers W runs W processes over every W-th line of the work list; each holds an exclusive lock on --gpu-lock
-(flock) from its first warm-up launch to its last timed event, so timed regions never overlap and only host work
-runs in parallel.  A/B of the two modes: re-time lines of an earlier single-process file with the same --stride /
+--workers W runs W processes over every W-th line of the work list, sharing a reader/writer lock on --gpu-lock
+(tools/gpu_rwlock.py): every GPU phase of a worker holds it shared, its warm-up and timed batches hold it exclusive,
+so no other worker's GPU work runs inside a timed region and only host work overlaps it.  A/B of the two modes: re-time lines of an earlier single-process file with the same --stride /
 --offset into another --out and compare the records' ms.
 
   python tools/sweep.py --dataset medium --stride 60 --k 1,8,32,128 --out gpurun_out/sweep_medium.jsonl
@@ -20,7 +20,7 @@ runs in parallel.  A/B of the two modes: re-time lines of an earlier single-proc
 from __future__ import annotations
 
 import argparse
-import fcntl
+import contextlib
 import json
 import os
 import subprocess
@@ -34,6 +34,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "spmm-research_amd"))
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tools"))
+from gpu_rwlock import GpuRWLock  # noqa: E402
 
 
 def twin_names() -> dict:
@@ -226,12 +227,13 @@ def main():
     ap.add_argument("--gold-rows", type=int, default=64, help="inexact sampled rows checked against the fp128 gold")
     ap.add_argument("--workers", type=int, default=1, help="host worker processes (timed regions serialised)")
     ap.add_argument("--worker", default=None, help=argparse.SUPPRESS)     # i/W: set by --workers
-    ap.add_argument("--gpu-lock", default=None, help="lock file serialising the timed regions of the workers")
-    ap.add_argument("--lock-alloc", action="store_true",
-                    help="also hold the GPU lock while a worker uploads A, allocates and fills B and C, and frees them: "
-                         "another worker's large allocations, fills and frees stretched a timed region by up to 2-3x "
-                         "on K=128 lines of > 10 M nonzeros (round 5); only the planner's host work and the checks "
-                         "then overlap a timed region")
+    ap.add_argument("--gpu-lock", default=None,
+                    help="lock file of a reader/writer GPU lock (tools/gpu_rwlock.py) shared by the workers: every phase "
+                         "that puts work on the GPU (upload, plan, B/C allocation and fills, checks, frees) holds it "
+                         "shared, a warm-up plus its timed batches hold it exclusive -- so no other worker's GPU work "
+                         "overlaps a timed region (round 5: other workers' allocations, fills and plans stretched timed "
+                         "regions up to 2-3x, DESIGN §6.29)")
+    ap.add_argument("--lock-alloc", action="store_true", help=argparse.SUPPRESS)   # round 5 flag; the lock covers it now
     ap.add_argument("--env", default="", help="ENV=V,ENV=V set while the engine plans (e.g. SPMM_HIP_MFMA=2)")
     ap.add_argument("--base-env", default=None,
                     help="A/B: also plan a baseline handle with these ENV=V,... (e.g. SPMM_HIP_MFMA=-1: the plan without "
@@ -310,7 +312,7 @@ def main():
     if args.worker is not None:
         wi_, wn_ = (int(x) for x in args.worker.split("/"))
         work = work[wi_::wn_]
-    lock_f = open(args.gpu_lock, "a+") if args.gpu_lock else None
+    lk = GpuRWLock(args.gpu_lock) if args.gpu_lock else None
 
     def prepare(line):
         t0 = time.time()
@@ -330,11 +332,9 @@ def main():
         t_wait = time.time() - tw
         fut = ex.submit(prepare, work[wi + 1][1]) if wi + 1 < len(work) else None
         try:
-            sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock_f, idx, line, todo, A, t_gen,
+            sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lk, idx, line, todo, A, t_gen,
                        t_wait, feat, dtypes)
         except (S.SpmmHipError, torch.OutOfMemoryError) as e:     # e.g. device memory held by other workers
-            if lock_f:
-                fcntl.flock(lock_f, fcntl.LOCK_UN)
             print(f"line {idx} skipped: {e}", flush=True)
         del A
         if args.worker is not None:
@@ -342,126 +342,134 @@ def main():
     ex.shutdown(cancel_futures=True)
 
 
-def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lock_f, idx, line, todo, A, t_gen, t_wait,
+def sweep_line(args, S, O, torch, dev, stream, sha, names, cores, rng, out, lk, idx, line, todo, A, t_gen, t_wait,
                feat, dtypes):
-    """Every requested (dtype, K) of one generated matrix: plan, time, check, append one record each."""
+    """Every requested (dtype, K) of one generated matrix: plan, time, check, append one record each.  With a GPU lock
+    (lk, tools/gpu_rwlock.py) every GPU phase holds it shared and the warm-up + timed batches hold it exclusive; the
+    handles are closed (and their device memory freed) whatever fails."""
+    shared = lk.shared if lk else contextlib.nullcontext
+    exclusive = lk.exclusive if lk else contextlib.nullcontext
     for dt in dtypes:
         dtype = np.float64 if dt == "f64" else np.float32
         tdtype = torch.float64 if dt == "f64" else torch.float32
         vals = A.values.astype(dtype)
-        tc = time.time()
-        if lock_f and args.lock_alloc:
-            fcntl.flock(lock_f, fcntl.LOCK_EX)
-        mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
-        mfb = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0) if args.base_env is not None else None
-        torch.cuda.synchronize()
-        if lock_f and args.lock_alloc:
-            fcntl.flock(lock_f, fcntl.LOCK_UN)
-        t_create = time.time() - tc
-        for dt2, k in todo:
-            if dt2 != dt:
-                continue
-            t0 = time.time()
-            with env_set(args.env):
-                mf.plan(k)
-            t_plan = time.time() - t0
-            if mfb is not None:
-                with env_set(args.base_env):
-                    mfb.plan(k)
-            if lock_f and args.lock_alloc:
-                fcntl.flock(lock_f, fcntl.LOCK_EX)
-            g = torch.Generator(device=dev)
-            g.manual_seed(42)
-            B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
-            Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
-            run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
-            Cb = runb = None
-            if mfb is not None:
-                Cb = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
-                runb = lambda: mfb.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cb.data_ptr(), k, stream.cuda_stream)  # noqa
-            torch.cuda.synchronize()
-            if lock_f and not args.lock_alloc:
-                fcntl.flock(lock_f, fcntl.LOCK_EX)
-
-            def timed(fn):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for _ in range(args.iters):
-                    fn()
-                e1.record(stream)
+        mf = mfb = None
+        try:
+            tc = time.time()
+            with shared():
+                mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
+                if args.base_env is not None:
+                    mfb = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, 0, 0)
                 torch.cuda.synchronize()
-                return e0.elapsed_time(e1) / args.iters
-            for _ in range(args.warmup):
-                run()
-                if runb is not None:
-                    runb()
-            ms_b, msb_b = [], []
-            t_wall = time.time()               # wall clock of the timed region (correlation with other activity)
-            for _ in range(args.batches):          # baseline and policy interleaved batch by batch
-                if runb is not None:
-                    msb_b.append(timed(runb))
-                ms_b.append(timed(run))
-            if lock_f:
-                fcntl.flock(lock_f, fcntl.LOCK_UN)
-            ms = min(ms_b)
-            t_timed = time.time() - t0 - t_plan
-            bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
-            t1 = time.time()
-            par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows(), args.gold_rows)
-            t_check = time.time() - t1
-            inf = mf.info()
-            rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
-                   "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
-                   "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9, "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12,
-                   "engine_sha256": sha, "batches": [round(x, 5) for x in ms_b], "t_wall": round(t_wall, 3), "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
-                   "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
-                   "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
-                   "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]), "tile_mode": mf.tile_info()["mode"],
-                   "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
-                              "timed": round(t_timed, 3), "check": round(t_check, 3)},
-                   **par}
-            if mfb is not None:
-                exb = mfb.exact_rows() & mf.exact_rows()
-                ext = torch.from_numpy(exb).to(dev)
-                it = torch.int64 if dt == "f64" else torch.int32
-                rec.update({"ms_base": min(msb_b), "batches_base": [round(x, 5) for x in msb_b],
-                            "speedup": min(msb_b) / ms, "base_env": args.base_env,
-                            "tile_mode_base": mfb.tile_info()["mode"],
-                            "bitexact_vs_base": bool(torch.equal(Cm[ext].view(it), Cb[ext].view(it)))})
-            if args.env:
-                rec["env"] = args.env
-            if rec["tile_mode"] != "none":
-                ti = mf.tile_info()
-                rec.update({"tile_rows": ti["rows"], "tile_nnz": ti["nnz"], "tile_chunks": ti["chunks"],
-                            "tile_reuse": ti["reuse"]})
-            if feat is not None:
-                rec["mem_mb"] = feat["mem_footprint"]
-                rec["features"] = {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled",
-                                                        "skew", "avg_num_neighbours", "cross_row_similarity")}
-            if args.cpu_baseline > 0:
-                x_col = np.ascontiguousarray(B.cpu().numpy().T).ravel()
-                rec.update(cpu_baseline(O, A, vals, x_col, k, args.cpu_baseline, cores))
-                rec["gpu_over_cpu"] = rec["gflops"] / rec["cpu_gflops"]
-            with open(out, "a") as f:
-                f.write(json.dumps(rec) + "\n")
-            print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
-                                                         "roofline_frac", "cpu_gflops", "speedup", "bitexact_seq_rows",
-                                                         "normwise_ok")}), flush=True)
-            if lock_f and args.lock_alloc:
-                fcntl.flock(lock_f, fcntl.LOCK_EX)
-            del B, Cm, Cb
-            torch.cuda.synchronize()
-            if args.worker is not None:
-                torch.cuda.empty_cache()
-            if lock_f and args.lock_alloc:
-                fcntl.flock(lock_f, fcntl.LOCK_UN)
-        if lock_f and args.lock_alloc:
-            fcntl.flock(lock_f, fcntl.LOCK_EX)
-        mf.close()
+            t_create = time.time() - tc
+            for dt2, k in todo:
+                if dt2 != dt:
+                    continue
+                sweep_k(args, S, O, torch, dev, stream, sha, names, cores, rng, out, shared, exclusive, idx, line, A,
+                        t_gen, t_wait, t_create, feat, dt, dtype, tdtype, vals, k, mf, mfb)
+        finally:
+            with shared():
+                if mf is not None:
+                    mf.close()
+                if mfb is not None:
+                    mfb.close()
+
+
+def sweep_k(args, S, O, torch, dev, stream, sha, names, cores, rng, out, shared, exclusive, idx, line, A, t_gen, t_wait,
+            t_create, feat, dt, dtype, tdtype, vals, k, mf, mfb):
+    """One (matrix, dtype, K) record."""
+    t0 = time.time()
+    with shared():
+        with env_set(args.env):
+            mf.plan(k)
+        t_plan = time.time() - t0
         if mfb is not None:
-            mfb.close()
-        if lock_f and args.lock_alloc:
-            fcntl.flock(lock_f, fcntl.LOCK_UN)
+            with env_set(args.base_env):
+                mfb.plan(k)
+        g = torch.Generator(device=dev)
+        g.manual_seed(42)
+        B = torch.rand((max(A.ncols, 1), k), generator=g, device=dev, dtype=tdtype)
+        Cm = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
+        Cb = runb = None
+        if mfb is not None:
+            Cb = torch.empty((max(A.m, 1), k), device=dev, dtype=tdtype)
+            runb = lambda: mfb.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cb.data_ptr(), k, stream.cuda_stream)  # noqa
+        torch.cuda.synchronize()
+    run = lambda: mf.spmm_device(B.data_ptr(), S.B_ROW_MAJOR, Cm.data_ptr(), k, stream.cuda_stream)  # noqa
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.iters):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.iters
+    ms_b, msb_b = [], []
+    with exclusive():
+        for _ in range(args.warmup):
+            run()
+            if runb is not None:
+                runb()
+        t_wall = time.time()               # wall clock of the timed region (correlation with other activity)
+        for _ in range(args.batches):          # baseline and policy interleaved batch by batch
+            if runb is not None:
+                msb_b.append(timed(runb))
+            ms_b.append(timed(run))
+    ms = min(ms_b)
+    t_timed = time.time() - t0 - t_plan
+    bytes_alg = S.bytes_alg(A.m, A.ncols, A.nnz, k, S.F64 if dtype == np.float64 else S.F32)
+    t1 = time.time()
+    with shared():
+        par = sample_parity(S, O, A, B, Cm, k, args.check_rows, rng, dtype, mf.exact_rows(), args.gold_rows)
+    t_check = time.time() - t1
+    inf = mf.info()
+    rec = {"gen": line, "idx": idx, "name": names.get(line), "k": k, "dtype": dt, "m": int(A.m),
+           "nnz": int(A.nnz), "ms": ms, "gflops": 2.0 * A.nnz * k / (ms * 1e-3) / 1e9,
+           "gbs_alg": bytes_alg / (ms * 1e-3) / 1e9, "roofline_frac": bytes_alg / (ms * 1e-3) / 8e12,
+           "engine_sha256": sha, "batches": [round(x, 5) for x in ms_b], "t_wall": round(t_wall, 3),
+           "gen_s": round(t_gen, 2), "seq_max": int(inf[8]), "cap": int(inf[9]),
+           "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
+           "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
+           "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
+           "tile_mode": mf.tile_info()["mode"],
+           "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
+                      "timed": round(t_timed, 3), "check": round(t_check, 3)},
+           **par}
+    if mfb is not None:
+        with shared():
+            exb = mfb.exact_rows() & mf.exact_rows()
+            ext = torch.from_numpy(exb).to(dev)
+            it = torch.int64 if dt == "f64" else torch.int32
+            rec.update({"ms_base": min(msb_b), "batches_base": [round(x, 5) for x in msb_b],
+                        "speedup": min(msb_b) / ms, "base_env": args.base_env,
+                        "tile_mode_base": mfb.tile_info()["mode"],
+                        "bitexact_vs_base": bool(torch.equal(Cm[ext].view(it), Cb[ext].view(it)))})
+    if args.env:
+        rec["env"] = args.env
+    if rec["tile_mode"] != "none":
+        ti = mf.tile_info()
+        rec.update({"tile_rows": ti["rows"], "tile_nnz": ti["nnz"], "tile_chunks": ti["chunks"],
+                    "tile_reuse": ti["reuse"]})
+    if feat is not None:
+        rec["mem_mb"] = feat["mem_footprint"]
+        rec["features"] = {x: feat[x] for x in ("avg_nnz_per_row", "std_nnz_per_row", "avg_bw_scaled",
+                                                "skew", "avg_num_neighbours", "cross_row_similarity")}
+    if args.cpu_baseline > 0:
+        with shared():
+            x_col = np.ascontiguousarray(B.cpu().numpy().T).ravel()
+        rec.update(cpu_baseline(O, A, vals, x_col, k, args.cpu_baseline, cores))
+        rec["gpu_over_cpu"] = rec["gflops"] / rec["cpu_gflops"]
+    with open(out, "a") as f:
+        f.write(json.dumps(rec) + "\n")
+    print(json.dumps({k2: rec.get(k2) for k2 in ("idx", "name", "k", "dtype", "ms", "gflops",
+                                                 "roofline_frac", "cpu_gflops", "speedup", "bitexact_seq_rows",
+                                                 "normwise_ok")}), flush=True)
+    with shared():
+        del B, Cm, Cb
+        torch.cuda.synchronize()
+        if args.worker is not None:
+            torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
