@@ -453,8 +453,7 @@ def run_lines(lines, K: int, dtype: str, iters: int, warmup: int, torch, S, np, 
         b = S.bytes_alg(A.m, A.ncols, A.nnz, K, dt_code)
         rec = {"gen": line, "m": int(A.m), "nnz": int(A.nnz), "ms": t * 1e3, "flops": 2.0 * A.nnz * K,
                "bytes_alg": b, "frac": b / t / 1e9 / HBM_PEAK_GBS, "gflops": 2.0 * A.nnz * K / t / 1e9,
-               "tiles": int(mf.info()[19]), "tile_mode": mf.tile_info()["mode"], "packed": mf.packed_rows(),
-               "selfcheck_ok": chk["ok"]}
+               "tiles": int(mf.info()[19]), "tile_mode": mf.tile_info()["mode"], "selfcheck_ok": chk["ok"]}
         if names:
             rec["name"] = names.get(line)
         pm = pmc.get(line)

@@ -157,10 +157,6 @@ int spmm_hip_tile_info(const spmm_hip_t *h, int64_t *out);
  * dense panels by v_mfma_f64_16x16x4_f64 -- the f64 MFMA is a chain of fused multiply-adds in k order, so these rows
  * are exact too).  SPMM_HIP_MFMA=-1 keeps the sparse tile kernel, 1 takes every eligible 16-row tile. */
 int spmm_hip_tile_mode(const spmm_hip_t *h);
-/* 1 when the current plan runs the row kernel's packed short rows (a row group gathers across the
- * ends of its short rows instead of one gather round trip per row; every row still one exact FMA chain), else 0
- * (multi-GPU handles: 1 when any shard does).  SPMM_HIP_PACK=-1 disables it, =1 packs every eligible plan. */
-int spmm_hip_packed_rows(const spmm_hip_t *h);
 
 /* Which C rows of the current plan are computed as ONE left-to-right FMA chain over the row in CSR order -- the
  * reference kernel's exact operation sequence, so bit-identical to it (mask[i] = 1); the others (rows longer than
@@ -266,7 +262,7 @@ void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t);
  * [10] split length T, [11] piece length of rows > T, [12] K-panel width, [13] K panels, [14] tiles built,
  * [15] nonzeros in tiles, [16] chunks, [17] row-kernel blocks, [18] split rows, [19] exact rows, [20] vector lanes,
  * [21] XCD order, [22] column windows, [23] 1 = gate only, [24]/[25] plan fingerprint (low / high 32 bits; two
- * plans are the same exactly when these agree), [26] est. taken tiles, [27] packed short rows. */
+ * plans are the same exactly when these agree), [26] est. taken tiles. */
 #define SPMM_HIP_PLAN_SLOTS 32
 int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t k,
                         int32_t dtype, int32_t mfma, int32_t gate_only, double *out);

@@ -165,10 +165,9 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     }
     // partial slots of this panel as one buffer resource (the fused path needs them below 4 GiB; checked at plan)
     const uint32_t pb = (uint32_t)std::min<uint64_t>((uint64_t)h->nslots * ld * sizeof(T), 0xFFFFFFFFull);
-    auto go = [&](auto mode_c, auto xcd_c, auto vl_c, auto pack_c) {
+    auto go = [&](auto mode_c, auto xcd_c, auto vl_c) {
         spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
-                         decltype(vl_c)::value, decltype(pack_c)::value>
-            <<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
+                         decltype(vl_c)::value><<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
             h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
             h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
     };
@@ -177,19 +176,12 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     using T_ = std::true_type;
     using F_ = std::false_type;
     const bool vl = h->plan.lmax > 1, sp = h->d_vdest != nullptr;   // split rows, or rows left to tiles
-    if constexpr (U > 0 && G > 1) {
-        if (h->plan.pack && !vl) {       // packed short rows: row-major order, no vector lanes
-            if (h->plan.xcd) sp ? go(split_c(), T_(), F_(), T_()) : go(row_c(), T_(), F_(), T_());
-            else sp ? go(split_c(), F_(), F_(), T_()) : go(row_c(), F_(), F_(), T_());
-            return;
-        }
-    }
     if (h->plan.xcd) {
-        if (sp) vl ? go(split_c(), T_(), T_(), F_()) : go(split_c(), T_(), F_(), F_());
-        else vl ? go(row_c(), T_(), T_(), F_()) : go(row_c(), T_(), F_(), F_());
+        if (sp) vl ? go(split_c(), T_(), T_()) : go(split_c(), T_(), F_());
+        else vl ? go(row_c(), T_(), T_()) : go(row_c(), T_(), F_());
     } else {
-        if (sp) vl ? go(split_c(), F_(), T_(), F_()) : go(split_c(), F_(), F_(), F_());
-        else vl ? go(row_c(), F_(), T_(), F_()) : go(row_c(), F_(), F_(), F_());
+        if (sp) vl ? go(split_c(), F_(), T_()) : go(split_c(), F_(), F_());
+        else vl ? go(row_c(), F_(), T_()) : go(row_c(), F_(), F_());
     }
 }
 
@@ -714,11 +706,6 @@ double window_bytes(double srow) {
 // 1.25x -- and not above (config 2 K=1, fill 0.4: 1.00x; 100 nnz/row K=8, fill 0.31: 0.93x; 500 nnz/row K=32, fill
 // 0.25: 0.65-0.99x), where it would only give up exact rows.
 constexpr double VL_ROW_FILL = 0.125;
-// packed short rows (spmm_kernels.hpp rows_packed): mean virtual-row length at most this many nonzeros
-// (rows shorter than a U = 16 gather batch), at least two rows per row group, sampled consecutive-row similarity below
-// PACK_MAX_CRS
-constexpr double PACK_MAX_ROW = 12.0;
-constexpr double PACK_MAX_CRS = 0.25;
 constexpr double VL_MIN_ROW = 32.0;   // mean virtual-row length (2 gather batches): tiny matrices stay exact
 
 // XCD-contiguous block order (policy).  The B rows an XCD's L2 must hold at a time are about one row span (the band
@@ -1437,18 +1424,6 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         }
         pl.exact_rows = 0;
         for (uint8_t e : d.exact) pl.exact_rows += e;
-        // packed short rows: a row group gathers across its rows' ends, so short rows stop paying a
-        // round trip each.  Rows of low consecutive-row similarity only (similar rows walked in step share their B
-        // lines within one gather instruction, which packing gives up); no vector lanes, no column windows, row
-        // groups of >= 2 lanes (one-lane groups hold 1-2 rows of a block).  SPMM_HIP_PACK=-1 off, 1 forced.
-        const int env_p = env_int("SPMM_HIP_PACK", 0);
-        const bool pack_ok = W == 0 && pl.lmax <= 1 && g >= 2 && nnz_rows > 0;
-        if (pack_ok && env_p > 0) {
-            pl.pack = 1;
-        } else if (pack_ok && env_p == 0 && mean_vrow <= PACK_MAX_ROW && rows_per_block >= 2.0 * ng) {
-            if (int st = load_cols()) return st;
-            pl.pack = crs < PACK_MAX_CRS ? 1 : 0;
-        }
     }
     // fused combine: split rows summed by the block that stores their last piece, so no combine
     // launch.  Needs one launch per panel (no column windows), partials below 4 GiB (32-bit buffer offsets) and each
@@ -1502,7 +1477,7 @@ uint64_t plan_fingerprint(const Draft &d) {
     const Plan &p = d.pl;
     const int64_t f[] = {p.k, p.kw, p.npanels, p.ygrid, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
                          p.xcd, p.lmax, p.exact_rows, p.ntile, p.tile_xcd, p.tile_wide, p.tile_mfma, p.tile_rows,
-                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse, p.pack};
+                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse};
     mix(f, sizeof(f));
     mix(d.in.vrow_ptr.data(), d.in.vrow_ptr.size() * 4);
     mix(d.in.vdest.data(), d.in.vdest.size() * 4);
@@ -2202,12 +2177,6 @@ int spmm_hip_tile_mode(const spmm_hip_t *h) {
     return h->plan.ntile == 0 ? 0 : h->plan.tile_mfma ? 2 : 1;
 }
 
-int spmm_hip_packed_rows(const spmm_hip_t *h) {
-    if (!h) return fail(SPMM_HIP_ERR_ARG, "packed_rows: bad handle");
-    if (h->multi) return multi_packed_rows(h);
-    return h->plan.pack ? 1 : 0;
-}
-
 int spmm_hip_exact_rows(const spmm_hip_t *h, uint8_t *mask) {
     if (!h || !mask || h->plan.k < 1) return fail(SPMM_HIP_ERR_ARG, "exact_rows: handle not planned");
     if (h->m > 0) std::memcpy(mask, h->exact.data(), (size_t)h->m);
@@ -2342,7 +2311,6 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     }
     out[23] = d.gate_only ? 1 : 0;
     out[26] = d.gate.tiles;
-    out[27] = p.pack;
     return SPMM_HIP_OK;
 }
 

@@ -43,7 +43,6 @@ struct Plan {
     int64_t nseg = 0;          // virtual rows (segments) over all windows
     int xcd = 0;               // 1 = XCD-contiguous block order (each XCD sweeps one eighth of the rows)
     int lmax = 1;              // vector lanes: max groups per row (1 = every row one group, exact)
-    int pack = 0;              // 1 = packed short rows: a row group gathers across its rows' ends (exact)
     int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
     int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
     int tile_xcd = 0;          // tiles in XCD-contiguous order
@@ -78,7 +77,6 @@ int multi_update_values(spmm_hip_t *h, const void *vals, bool device, hipStream_
 int multi_last_times(spmm_hip_t *h, double *out_ms);
 void multi_info(const spmm_hip_t *h, int64_t *out);
 int multi_tile_mode(const spmm_hip_t *h);
-int multi_packed_rows(const spmm_hip_t *h);
 void multi_destroy(spmm_hip_t *h);
 
 }  // namespace spmm_engine

@@ -283,67 +283,8 @@ __device__ __forceinline__ int xcd_block(int w, int nb) {
 // rows of blocks with L > 1 are reported as inexact (spmm_hip_exact_rows).  L is block-uniform; L = 1 blocks are
 // exactly the plain kernel.  Only blocks flagged by the inspector (bit 30 of blk.y: all blocks when the matrix-wide
 // policy chose vector lanes, else blocks made only of split-row pieces, which are inexact anyway) may use L > 1.
-// PACK (round 6, short rows): a row group walks the nonzeros of ITS rows (grp, grp + NG, ...) as one stream and
-// issues U gathers per batch across row ends, instead of one batch per row -- a 5-nonzero row otherwise costs a
-// whole gather round trip for 5 gathers, and a group's ~13 rows of a block run as 13 serial round trips (DESIGN
-// §6.32).  Each row is still one FMA chain from 0 in CSR order (bit-identical); empty rows are stored first.  Only
-// for DEST_ROW / DEST_SPLIT without vector lanes.  Trade-off: the groups of a wave no longer start every row in step,
-// so the texture unit stops merging the same column of adjacent similar rows -- the policy packs low-similarity
-// rows only.
-template <typename T, int VEC, int U, int MODE, bool NTC, typename Gather, typename StoreRow>
-__device__ __forceinline__ void rows_packed(const int32_t *s_rp, const int32_t *s_col, const T *s_val, int jb, int grp,
-                                            int rstep, int nrows, const Gather &gather, const StoreRow &store_row) {
-    using V = vec<T, VEC>;
-    for (int r = grp; r < nrows; r += rstep)
-        if (s_rp[r] == s_rp[r + 1]) store_row(r, vzero<T, VEC>());
-    auto next_row = [&](int rr) {
-        while (rr < nrows && s_rp[rr] == s_rp[rr + 1]) rr += rstep;
-        return rr;
-    };
-    int r = next_row(grp);              // row of the next nonzero to gather
-    int j = 0, e = 0;
-    if (r < nrows) j = s_rp[r] - jb, e = s_rp[r + 1] - jb;
-    int cr = r;                         // row being accumulated
-    V acc = vzero<T, VEC>();
-    while (r < nrows) {
-        V bv[U];
-        int jp[U];
-        uint32_t first = 0;             // bit u: gather u starts the next row of the stream
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            jp[u] = -1;
-            if (r < nrows) {
-                if (j == e) {
-                    r = next_row(r + rstep);
-                    if (r < nrows) {
-                        j = s_rp[r] - jb, e = s_rp[r + 1] - jb;
-                        first |= 1u << u;
-                    }
-                }
-                if (r < nrows) {
-                    jp[u] = j;
-                    bv[u] = gather(s_col[j]);
-                    ++j;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (jp[u] >= 0) {
-                if (first & (1u << u)) {
-                    store_row(cr, acc);
-                    acc = vzero<T, VEC>();
-                    cr = next_row(cr + rstep);
-                }
-                vfma(acc, s_val[jp[u]], bv[u]);
-            }
-        }
-    }
-    if (cr < nrows) store_row(cr, acc);
-}
-
 template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE, bool XCD = false,
-          bool VL = false, bool PACK = false>
+          bool VL = false>
 __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
@@ -461,21 +402,6 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
         const int kk = kc + lane * VEC;
         if (kk >= kw) continue;
         const BGather<T, VEC, BUF> gather(B, kk, ld, b_bytes);
-        if constexpr (PACK && !VL && MODE != DEST_CHAIN && U > 0) {
-            auto store_row = [&](int r, const vec<T, VEC> &acc) {
-                if constexpr (MODE == DEST_SPLIT) {
-                    const int d = vdest[r0 + r];
-                    if (fuse && d < 0)
-                        vstore_sc1<T, VEC>(prs, (uint32_t)(((size_t)(-d - 1) * ld + kk) * sizeof(T)), acc);
-                    else
-                        vstore<T, VEC, NTC>(((d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld) + kk, acc);
-                } else {
-                    vstore<T, VEC, NTC>(C + (size_t)(r0 + r) * ld + kk, acc);
-                }
-            };
-            rows_packed<T, VEC, U, MODE, NTC>(s_rp, s_col, s_val, jb, grp, rstep, nrows, gather, store_row);
-            continue;
-        }
         for (int r = grp; r < nrows; r += rstep) {
             T *dst;
             V acc = vzero<T, VEC>();

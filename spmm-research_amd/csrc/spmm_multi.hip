@@ -336,13 +336,6 @@ int multi_tile_mode(const spmm_hip_t *h) {
     return mode;
 }
 
-// Packed short rows: 1 when any shard's plan packs them.
-int multi_packed_rows(const spmm_hip_t *h) {
-    int any = 0;
-    for (const spmm_hip_t *c : h->multi->shard) any = std::max(any, spmm_hip_packed_rows(c));
-    return any;
-}
-
 void multi_destroy(spmm_hip_t *h) {
     MultiState *M = h->multi;
     if (!M) return;

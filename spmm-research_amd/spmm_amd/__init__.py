@@ -129,7 +129,6 @@ def _bind_hip(L: C.CDLL) -> C.CDLL:
     L.spmm_hip_debug_free.restype = None
     L.spmm_hip_tile_info.argtypes = [vp, np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")]
     L.spmm_hip_tile_mode.argtypes = [vp]
-    L.spmm_hip_packed_rows.argtypes = [vp]
     L.spmm_hip_run_rowmajor.argtypes = [vp, vp, vp, i32]
     L.spmm_hip_update_values.argtypes = [vp, vp]
     L.spmm_hip_update_values_device.argtypes = [vp, vp, vp]
@@ -539,13 +538,6 @@ class MatrixFormat:
         return {"tiles": int(out[0]), "rows": int(out[1]), "nnz": int(out[2]), "chunks": int(out[3]),
                 "reuse": out[4] / 1000.0, "xcd": int(out[5]), "wide": int(out[6]),
                 "mode": {0: "none", 1: "lds", 2: "mfma"}.get(mode, "none")}
-
-    def packed_rows(self) -> bool:
-        """The plan runs the row kernel's packed short rows (spmm_hip_packed_rows)."""
-        r = hip.spmm_hip_packed_rows(self._h)
-        if r < 0:
-            _check("packed_rows", r)
-        return bool(r)
 
     def exact_rows(self) -> np.ndarray:
         """bool[m]: rows computed as the reference's single left-to-right FMA chain (bit-identical to it)."""

@@ -61,8 +61,7 @@ def main():
                 inf = mf.info()
                 print(json.dumps({"gen": line, "k": k, "plan": name, "dtype": args.dtype,
                                   "ms": round(e0.elapsed_time(e1) / args.launches, 5),
-                                  "tile": mf.tile_info(), "packed": mf.packed_rows(),
-                                  "info": [int(v) for v in inf]}), flush=True)
+                                  "tile": mf.tile_info(), "info": [int(v) for v in inf]}), flush=True)
                 mf.close()
             del B, C
 

@@ -432,7 +432,7 @@ def sweep_k(args, S, O, torch, dev, stream, sha, names, cores, rng, out, shared,
            "panel_k": int(inf[10]), "split_rows": int(inf[6]), "blocks": int(inf[5]),
            "windows": int(inf[12]), "win_cols": int(inf[13]), "segments": int(inf[14]),
            "xcd": int(inf[15]), "lmax": int(inf[16]), "exact_rows": int(inf[17]), "tiles": int(inf[19]),
-           "tile_mode": mf.tile_info()["mode"], "packed": mf.packed_rows(),
+           "tile_mode": mf.tile_info()["mode"],
            "host_s": {"wait_gen": round(t_wait, 3), "create": round(t_create, 3), "plan": round(t_plan, 3),
                       "timed": round(t_timed, 3), "check": round(t_check, 3)},
            **par}
