@@ -119,6 +119,8 @@ def parse():
                     help="override the config-4 generator line (the strong-split sub-record; tests use a small one)")
     ap.add_argument("--dump-c-strong", default=None, help="rank 0 writes a row sample of the config-4 record's C (npz)")
     ap.add_argument("--dataset-stride", type=int, default=80, help="dataset: every n-th medium-dataset line")
+    ap.add_argument("--dataset-out", default=None,
+                    help="write the dataset pass's per-matrix records (JSONL; rank r appends .r<r> at N > 1)")
     ap.add_argument("--dataset-offset", type=int, default=0)
     ap.add_argument("--dataset-iters", type=int, default=10, help="dataset / twins: timed launches per matrix")
     ap.add_argument("--dataset-warmup", type=int, default=3)
@@ -548,6 +550,12 @@ def run_dataset_record(args, torch, S, np, iters: int | None = None, warmup: int
     res = run_lines(lines, args.k, args.dtype, iters, warmup, torch, S, np,
                     cpu_budget_s=0.0 if (args.no_cpu_baseline or not cpu) else args.dataset_cpu_seconds, pmc=pmc)
     rec = summarize(res, args.k)
+    if args.dataset_out:
+        rank = int(os.environ.get("RANK", "0"))
+        path = args.dataset_out + (f".r{rank}" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "")
+        with open(path, "w") as f:
+            for r in res["recs"]:
+                f.write(json.dumps(r) + "\n")
     rec.update({"metric": METRIC, "scaling": "single-gpu", "dtype": args.dtype,
                 "workload": f"every {args.dataset_stride}th line of synthetic_matrices_medium_dataset from "
                             f"{offset} ({len(lines)} matrices), K={args.k}",

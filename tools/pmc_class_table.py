@@ -53,8 +53,7 @@ def main():
     rc = args.recompute
     print("| avg | bw | matrices | frac of ceiling: median (p10–p90) | " + ("gather-only ceiling (r05) median | " if rc
                                                                           else "")
-          + "compulsory frac median | past-L2 / alg bytes | L2 hit | bound: gather / L2 req" + (" / HBM" if rc else "")
-          + " | with tiles |")
+          + "compulsory frac median | past-L2 / alg bytes | L2 hit | bound: gather / L2 req / HBM | with tiles |")
     print("|---|---|---|---|---|---|---|---|---|" + ("---|" if rc else ""))
     allf = []
     for key in sorted(cls):
@@ -70,8 +69,7 @@ def main():
         nh = sum(1 for r in rs if r.get("achievable_bound") == "HBM compulsory")
         old_ = (f"{np.median([r['frac_of_achievable_r05'] for r in rs]):.2f} | " if rc else "")
         print(f"| {key[0]} | {key[1]} | {len(rs)} | {np.median(fa):.2f} ({np.percentile(fa, 10):.2f}–"
-              f"{np.percentile(fa, 90):.2f}) | {old_}{fr:.3f} | {tr:.2f} | {hit:.2f} | {ng} / {nb}"
-              + (f" / {nh}" if rc else "") + f" | {nt} |")
+              f"{np.percentile(fa, 90):.2f}) | {old_}{fr:.3f} | {tr:.2f} | {hit:.2f} | {ng} / {nb} / {nh} | {nt} |")
     allf = np.array(allf)
     old_all = (f"{np.median([r['frac_of_achievable_r05'] for r in recs.values()]):.2f} | " if rc else "")
     print(f"| **all** | | {len(recs)} | **{np.median(allf):.2f}** ({np.percentile(allf, 10):.2f}–"

@@ -184,7 +184,7 @@ def collect(args):
             rd = 2.0 * res[1][j]["FETCH_SIZE"] * 1024 / L
             wr = res[2][j]["WRITE_SIZE"] * 1024 / L
             hit, miss = res[2][j].get("TCC_HIT_sum", 0.0) / L, res[2][j].get("TCC_MISS_sum", 0.0) / L
-            ach = bench.achievable(ms, rd + wr, hit + miss, float(mrec["ncols"]) * args.k * s)
+            ach = bench.achievable(ms, rd + wr, hit + miss, float(mrec["ncols"]) * args.k * s, mrec["bytes_alg"])
             rec = {**mrec, "k": args.k, "dtype": args.dtype, "engine_sha256": sha, "kernel_ms": ms,
                    "kernel_sum_ms": res[0][j]["ns"] / L / 1e6,
                    "gflops": 2.0 * mrec["nnz"] * args.k / (ms * 1e-3) / 1e9,
