@@ -165,9 +165,10 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     }
     // partial slots of this panel as one buffer resource (the fused path needs them below 4 GiB; checked at plan)
     const uint32_t pb = (uint32_t)std::min<uint64_t>((uint64_t)h->nslots * ld * sizeof(T), 0xFFFFFFFFull);
-    auto go = [&](auto mode_c, auto xcd_c, auto vl_c) {
+    auto go = [&](auto mode_c, auto xcd_c, auto vl_c, auto pair_c) {
         spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
-                         decltype(vl_c)::value><<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
+                         decltype(vl_c)::value, decltype(pair_c)::value>
+            <<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
             h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
             h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
     };
@@ -176,12 +177,24 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     using T_ = std::true_type;
     using F_ = std::false_type;
     const bool vl = h->plan.lmax > 1, sp = h->d_vdest != nullptr;   // split rows, or rows left to tiles
+    if constexpr (U > 1 && G > 1) {
+        if (h->plan.pair) {              // paired short rows
+            if (h->plan.xcd) {
+                if (sp) vl ? go(split_c(), T_(), T_(), T_()) : go(split_c(), T_(), F_(), T_());
+                else vl ? go(row_c(), T_(), T_(), T_()) : go(row_c(), T_(), F_(), T_());
+            } else {
+                if (sp) vl ? go(split_c(), F_(), T_(), T_()) : go(split_c(), F_(), F_(), T_());
+                else vl ? go(row_c(), F_(), T_(), T_()) : go(row_c(), F_(), F_(), T_());
+            }
+            return;
+        }
+    }
     if (h->plan.xcd) {
-        if (sp) vl ? go(split_c(), T_(), T_()) : go(split_c(), T_(), F_());
-        else vl ? go(row_c(), T_(), T_()) : go(row_c(), T_(), F_());
+        if (sp) vl ? go(split_c(), T_(), T_(), F_()) : go(split_c(), T_(), F_(), F_());
+        else vl ? go(row_c(), T_(), T_(), F_()) : go(row_c(), T_(), F_(), F_());
     } else {
-        if (sp) vl ? go(split_c(), F_(), T_()) : go(split_c(), F_(), F_());
-        else vl ? go(row_c(), F_(), T_()) : go(row_c(), F_(), F_());
+        if (sp) vl ? go(split_c(), F_(), T_(), F_()) : go(split_c(), F_(), F_(), F_());
+        else vl ? go(row_c(), F_(), T_(), F_()) : go(row_c(), F_(), F_(), F_());
     }
 }
 
@@ -706,6 +719,17 @@ double window_bytes(double srow) {
 // 1.25x -- and not above (config 2 K=1, fill 0.4: 1.00x; 100 nnz/row K=8, fill 0.31: 0.93x; 500 nnz/row K=32, fill
 // 0.25: 0.65-0.99x), where it would only give up exact rows.
 constexpr double VL_ROW_FILL = 0.125;
+// paired short rows (spmm_kernels.hpp rows_pair_step), policy: fp64 (fp32 K = 32 measured neutral),
+// mean virtual-row length at most PAIR_MAX_ROW nonzeros, at least two rows per row group, row groups of at most
+// PAIR_MAX_G lanes (K <= 32: 64-lane groups lost up to 10 %), at least PAIR_MIN_NNZ nonzeros (smaller launches lost
+// up to 8 %), and neighbouring rows that share columns (sampled reuse of 16-row windows, nonzeros per distinct
+// column, at least PAIR_MIN_REUSE: rows with nothing in common gained nothing).  Fitted on 19 avg-5 lines, checked
+// on 60 others (profiles/r06/pair/).
+constexpr double PAIR_MAX_ROW = 6.0;
+constexpr int PAIR_MAX_G = 16;
+constexpr double PAIR_MIN_REUSE = 2.0;
+constexpr int PAIR_WINDOW_ROWS = 16;
+constexpr int64_t PAIR_MIN_NNZ = 4 << 20;
 constexpr double VL_MIN_ROW = 32.0;   // mean virtual-row length (2 gather batches): tiny matrices stay exact
 
 // XCD-contiguous block order (policy).  The B rows an XCD's L2 must hold at a time are about one row span (the band
@@ -1424,6 +1448,19 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         }
         pl.exact_rows = 0;
         for (uint8_t e : d.exact) pl.exact_rows += e;
+        // paired short rows: two rows of <= U/2 nonzeros share a gather round trip, the wave's groups
+        // still in step.  No column windows, row groups of >= 2 lanes (one-lane groups hold 1-2 rows of a block);
+        // blocks that take vector lanes keep their loop.  SPMM_HIP_PAIR=-1 off, 1 forced.
+        const int env_pair = env_int("SPMM_HIP_PAIR", 0);
+        const bool pair_ok = W == 0 && g >= 2 && nnz_rows > 0;
+        if (pair_ok && env_pair > 0)
+            pl.pair = 1;
+        else if (pair_ok && env_pair == 0 && h->vsize == 8 && g <= PAIR_MAX_G && h->nnz >= PAIR_MIN_NNZ &&
+                 mean_vrow <= PAIR_MAX_ROW && rows_per_block >= 2.0 * ng) {
+            if (int st = load_cols()) return st;
+            pl.pair_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, INT32_MAX, PAIR_WINDOW_ROWS);
+            if (pl.pair_reuse >= PAIR_MIN_REUSE) pl.pair = 1;
+        }
     }
     // fused combine: split rows summed by the block that stores their last piece, so no combine
     // launch.  Needs one launch per panel (no column windows), partials below 4 GiB (32-bit buffer offsets) and each
@@ -1477,7 +1514,7 @@ uint64_t plan_fingerprint(const Draft &d) {
     const Plan &p = d.pl;
     const int64_t f[] = {p.k, p.kw, p.npanels, p.ygrid, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
                          p.xcd, p.lmax, p.exact_rows, p.ntile, p.tile_xcd, p.tile_wide, p.tile_mfma, p.tile_rows,
-                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse};
+                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse, p.pair};
     mix(f, sizeof(f));
     mix(d.in.vrow_ptr.data(), d.in.vrow_ptr.size() * 4);
     mix(d.in.vdest.data(), d.in.vdest.size() * 4);
@@ -2311,6 +2348,8 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     }
     out[23] = d.gate_only ? 1 : 0;
     out[26] = d.gate.tiles;
+    out[27] = p.pair;
+    out[28] = p.pair_reuse;
     return SPMM_HIP_OK;
 }
 

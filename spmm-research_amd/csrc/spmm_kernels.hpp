@@ -283,8 +283,48 @@ __device__ __forceinline__ int xcd_block(int w, int nb) {
 // rows of blocks with L > 1 are reported as inexact (spmm_hip_exact_rows).  L is block-uniform; L = 1 blocks are
 // exactly the plain kernel.  Only blocks flagged by the inspector (bit 30 of blk.y: all blocks when the matrix-wide
 // policy chose vector lanes, else blocks made only of split-row pieces, which are inexact anyway) may use L > 1.
+// PAIR (round 6, short rows): a row group takes its rows two at a time -- row r in gather slots 0..U/2-1,
+// row r + NG in slots U/2..U-1 -- so two short rows share one gather round trip.  The four groups of a wave keep
+// walking ADJACENT rows at the SAME slots (r, r+1, r+2, r+3 in the first half, the rows NG further in the second), so
+// the texture unit still merges the B lines that similar neighbouring rows share (the in-step merge of DESIGN §6.31,
+// which the packed stream of §6.32 lost).  A pair step is taken only when every group of the wave has both its rows
+// within U/2 nonzeros (a wave vote, so the branch is uniform); otherwise the two rows run the plain per-row loop.
+// Every row is still one FMA chain from 0 in CSR order (bit-identical).  DEST_ROW / DEST_SPLIT; blocks that take
+// vector lanes (split-row pieces) run their own loop.
+template <typename T, int VEC, int U, typename Gather, typename Init, typename Store>
+__device__ __forceinline__ bool rows_pair_step(const int32_t *s_rp, const int32_t *s_col, const T *s_val, int jb,
+                                               int r, int r2, int nrows, const Gather &gather, const Init &init,
+                                               const Store &store) {
+    using V = vec<T, VEC>;
+    constexpr int H = U / 2;
+    const int a0 = s_rp[r] - jb, e0 = s_rp[r + 1] - jb;
+    const bool two = r2 < nrows;
+    const int a1 = two ? s_rp[r2] - jb : 0, e1 = two ? s_rp[r2 + 1] - jb : 0;
+    if (!__all(e0 - a0 <= H && e1 - a1 <= H)) return false;
+    V bv[U];
+#pragma unroll
+    for (int u = 0; u < H; ++u)
+        if (a0 + u < e0) bv[u] = gather(s_col[a0 + u]);
+#pragma unroll
+    for (int u = 0; u < H; ++u)
+        if (a1 + u < e1) bv[H + u] = gather(s_col[a1 + u]);
+    V acc0 = init(r);
+#pragma unroll
+    for (int u = 0; u < H; ++u)
+        if (a0 + u < e0) vfma(acc0, s_val[a0 + u], bv[u]);
+    store(r, acc0);
+    if (two) {
+        V acc1 = init(r2);
+#pragma unroll
+        for (int u = 0; u < H; ++u)
+            if (a1 + u < e1) vfma(acc1, s_val[a1 + u], bv[H + u]);
+        store(r2, acc1);
+    }
+    return true;
+}
+
 template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE, bool XCD = false,
-          bool VL = false>
+          bool VL = false, bool PAIR = false>
 __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
@@ -402,6 +442,29 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
         const int kk = kc + lane * VEC;
         if (kk >= kw) continue;
         const BGather<T, VEC, BUF> gather(B, kk, ld, b_bytes);
+        if constexpr (PAIR && MODE != DEST_CHAIN && U > 1) if (L == 1) {   // L: block-uniform (vector-lane blocks below)
+            auto init = [&](int) { return vzero<T, VEC>(); };
+            auto store_row = [&](int r, const vec<T, VEC> &acc) {
+                if constexpr (MODE == DEST_SPLIT) {
+                    const int d = vdest[r0 + r];
+                    if (fuse && d < 0)
+                        vstore_sc1<T, VEC>(prs, (uint32_t)(((size_t)(-d - 1) * ld + kk) * sizeof(T)), acc);
+                    else
+                        vstore<T, VEC, NTC>(((d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld) + kk, acc);
+                } else {
+                    vstore<T, VEC, NTC>(C + (size_t)(r0 + r) * ld + kk, acc);
+                }
+            };
+            for (int r = grp; r < nrows; r += 2 * rstep) {
+                const int r2 = r + rstep;
+                if (rows_pair_step<T, VEC, U>(s_rp, s_col, s_val, jb, r, r2, nrows, gather, init, store_row)) continue;
+                store_row(r, row_dot<T, VEC, U>(vzero<T, VEC>(), s_col, s_val, s_rp[r] - jb, s_rp[r + 1] - jb, gather));
+                if (r2 < nrows)
+                    store_row(r2, row_dot<T, VEC, U>(vzero<T, VEC>(), s_col, s_val, s_rp[r2] - jb, s_rp[r2 + 1] - jb,
+                                                     gather));
+            }
+            continue;
+        }
         for (int r = grp; r < nrows; r += rstep) {
             T *dst;
             V acc = vzero<T, VEC>();
