@@ -17,7 +17,7 @@ import json
 
 import numpy as np
 
-ENGINE = ("spmm_rows_kernel", "spmm_tile_kernel", "spmm_mfma_tile_kernel", "spmm_combine_kernel", "mfma_range_kernel",
+ENGINE = ("spmm_rows_kernel", "spmm_ring_kernel", "spmm_tile_kernel", "spmm_mfma_tile_kernel", "spmm_combine_kernel", "mfma_range_kernel",
           "mfma_fixup_kernel")
 
 
