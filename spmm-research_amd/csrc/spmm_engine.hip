@@ -201,45 +201,6 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
 // 32-bit buffer offsets for the B gather are valid while B fits 4 GiB.
 inline bool buf_ok(const spmm_hip_t *h, int ld) { return (uint64_t)h->ncols * (uint64_t)ld * h->vsize < (1ULL << 32); }
 
-// Streamed rows (spmm_ring_kernel): NG consecutive virtual rows per workgroup, one per row group;
-// 16-byte lanes, groups of >= 4 lanes, one pass over the panel and buffer-offset gathers (all checked at plan).
-template <typename T, int G>
-void launch_ring_g(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
-    constexpr int VEC = 16 / (int)sizeof(T);
-    constexpr int NG = WG / G;
-    const uint32_t bb = (uint32_t)std::min<uint64_t>((uint64_t)h->ncols * ld * sizeof(T), 0xFFFFFFFFull);
-    const dim3 grid((unsigned)((h->nv + NG - 1) / NG), h->plan.ygrid ? h->plan.npanels : 1);
-    auto go = [&](auto mode_c, auto xcd_c) {
-        auto run = [&](auto u_c) {
-            spmm_ring_kernel<T, VEC, G, decltype(u_c)::value, (bool)DEF_NTC, true, decltype(mode_c)::value,
-                             decltype(xcd_c)::value>
-                <<<grid, WG, 0, s>>>(h->d_vrow_ptr, h->d_col, (const T *)h->d_val, (int)h->nv, h->d_vdest, B, C, P,
-                                     ld, kw, bb, (int)h->nnz);
-        };
-        if (h->plan.ring == 2) run(std::integral_constant<int, 32>());
-        else if (h->plan.ring == 3) run(std::integral_constant<int, -16>());
-        else run(std::integral_constant<int, DEF_U>());
-    };
-    using split_c = std::integral_constant<int, DEST_SPLIT>;
-    using row_c = std::integral_constant<int, DEST_ROW>;
-    const bool sp = h->d_vdest != nullptr;
-    if (h->plan.xcd) sp ? go(split_c(), std::true_type()) : go(row_c(), std::true_type());
-    else sp ? go(split_c(), std::false_type()) : go(row_c(), std::false_type());
-}
-
-template <typename T>
-void launch_ring(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStream_t s) {
-    int vec, g;
-    lane_layout(kw, ld, sizeof(T), vec, g);
-    switch (g) {
-        case 4: launch_ring_g<T, 4>(h, B, C, P, ld, kw, s); break;
-        case 8: launch_ring_g<T, 8>(h, B, C, P, ld, kw, s); break;
-        case 16: launch_ring_g<T, 16>(h, B, C, P, ld, kw, s); break;
-        case 32: launch_ring_g<T, 32>(h, B, C, P, ld, kw, s); break;
-        default: launch_ring_g<T, 64>(h, B, C, P, ld, kw, s); break;
-    }
-}
-
 #ifdef SPMM_TUNING
 // Tuning build only: a grid of row-kernel variants for the fp64 16-byte-lane shapes, selected at run time.
 template <typename T, int VEC, int G, int U, bool NTC, bool DMA, bool BUF>
@@ -409,10 +370,7 @@ void launch_spmm_t(spmm_hip_t *h, const T *B, T *C, int K, hipStream_t s, hipStr
         const int k0 = p * h->plan.kw;
         const int kw = std::min(h->plan.kw, K - k0);
         // ygrid: every panel of the row kernel in one launch (blockIdx.y = panel; equal panel widths, checked at plan)
-        if (h->nblk > 0 && (!h->plan.ygrid || p == 0)) {
-            if (h->plan.ring) launch_ring<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
-            else launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
-        }
+        if (h->nblk > 0 && (!h->plan.ygrid || p == 0)) launch_panel<T>(h, B + k0, C + k0, P ? P + k0 : nullptr, K, kw, rs);
         if (h->plan.ntile > 0 && !h->plan.tile_mfma) launch_tiles<T>(h, B + k0, C + k0, K, kw, s);
     }
     if (h->nlong > 0 && !h->fuse) {
@@ -772,11 +730,6 @@ constexpr int PAIR_MAX_G = 16;
 constexpr double PAIR_MIN_REUSE = 2.0;
 constexpr int PAIR_WINDOW_ROWS = 16;
 constexpr int64_t PAIR_MIN_NNZ = 4 << 20;
-// streamed rows (spmm_ring_kernel): policy switch and its shape rule (mean virtual row, staged rows
-// per block against row groups)
-constexpr bool RING_POLICY = false;
-constexpr double RING_MIN_ROW = 128.0;
-constexpr double RING_ROW_FILL = 0.5;
 constexpr double VL_MIN_ROW = 32.0;   // mean virtual-row length (2 gather batches): tiny matrices stay exact
 
 // XCD-contiguous block order (policy).  The B rows an XCD's L2 must hold at a time are about one row span (the band
@@ -1453,20 +1406,8 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         const double nnz_rows = (double)(h->nnz - (tiles ? tp.nnz : 0));
         const double rows_per_block = in.blk.empty() ? 0.0 : nvr / (double)nblk;
         const double mean_vrow = nvr > 0 ? nnz_rows / nvr : 0.0;
-        // streamed rows: one virtual row per row group, A streamed through LDS -- for long rows, where
-        // a staged block holds fewer rows than row groups.  No column windows, tiles or vector lanes; 16-byte lanes,
-        // groups of >= 4 lanes, one pass over the panel.  SPMM_HIP_RING=-1 off, 1 forced where the shape allows, 2
-        // forced with 32 gathers in flight per row, 3 forced with the software-pipelined row.
-        {
-            const int env_r = env_int("SPMM_HIP_RING", 0);
-            const bool ring_ok = W == 0 && !tiles && in.ngaps == 0 && g >= 4 && vec * (int)h->vsize == 16 &&
-                                 pl.kw <= g * vec && nnz_rows > 0 && buf_ok(h, k) && nvr < (double)INT32_MAX;
-            if (ring_ok && (env_r > 0 || (env_r == 0 && RING_POLICY && mean_vrow >= RING_MIN_ROW &&
-                                          rows_per_block <= RING_ROW_FILL * ng)))
-                pl.ring = env_r == 2 || env_r == 3 ? env_r : 1;
-        }
         const int env_l = env_int("SPMM_HIP_LANES", 0);
-        const int forced = pl.ring ? -1 : h->var.lanes != 0 ? h->var.lanes : env_l;
+        const int forced = h->var.lanes != 0 ? h->var.lanes : env_l;
         bool all_blocks = false;
         if (forced != 0)
             all_blocks = forced > 0, pl.lmax = forced > 0 ? std::min(forced, lcap) : 1;
@@ -1511,7 +1452,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         // still in step.  No column windows, row groups of >= 2 lanes (one-lane groups hold 1-2 rows of a block);
         // blocks that take vector lanes keep their loop.  SPMM_HIP_PAIR=-1 off, 1 forced.
         const int env_pair = env_int("SPMM_HIP_PAIR", 0);
-        const bool pair_ok = W == 0 && g >= 2 && nnz_rows > 0 && !pl.ring;
+        const bool pair_ok = W == 0 && g >= 2 && nnz_rows > 0;
         if (pair_ok && env_pair > 0)
             pl.pair = 1;
         else if (pair_ok && env_pair == 0 && h->vsize == 8 && g <= PAIR_MAX_G && h->nnz >= PAIR_MIN_NNZ &&
@@ -1528,7 +1469,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
     {
         std::vector<int32_t> &slot_lr = d.slot_lr;
         const int nslots = in.nslots;
-        bool fuse = nslots > 0 && W == 0 && !pl.ygrid && !pl.ring && env_int("SPMM_HIP_FUSE", 1) != 0 &&
+        bool fuse = nslots > 0 && W == 0 && !pl.ygrid && env_int("SPMM_HIP_FUSE", 1) != 0 &&
                     (uint64_t)nslots * (uint64_t)k * h->vsize < (1ULL << 32);
         if (fuse) {
             slot_lr.assign((size_t)nslots, -1);
@@ -1573,7 +1514,7 @@ uint64_t plan_fingerprint(const Draft &d) {
     const Plan &p = d.pl;
     const int64_t f[] = {p.k, p.kw, p.npanels, p.ygrid, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
                          p.xcd, p.lmax, p.exact_rows, p.ntile, p.tile_xcd, p.tile_wide, p.tile_mfma, p.tile_rows,
-                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse, p.pair, p.ring};
+                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse, p.pair};
     mix(f, sizeof(f));
     mix(d.in.vrow_ptr.data(), d.in.vrow_ptr.size() * 4);
     mix(d.in.vdest.data(), d.in.vdest.size() * 4);
@@ -2409,7 +2350,6 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     out[26] = d.gate.tiles;
     out[27] = p.pair;
     out[28] = p.pair_reuse;
-    out[29] = p.ring;
     return SPMM_HIP_OK;
 }
 

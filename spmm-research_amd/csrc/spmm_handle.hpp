@@ -45,7 +45,6 @@ struct Plan {
     int lmax = 1;              // vector lanes: max groups per row (1 = every row one group, exact)
     int pair = 0;              // 1 = paired short rows: two rows of <= U/2 nonzeros per gather batch (exact)
     double pair_reuse = 0.0;   // the pair policy's sampled 16-row-window reuse (0 = not sampled)
-    int ring = 0;              // 1 = streamed rows (spmm_ring_kernel): one virtual row per row group, A through LDS
     int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
     int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
     int tile_xcd = 0;          // tiles in XCD-contiguous order

@@ -553,101 +553,6 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
     }
 }
 
-// ------------------------------------------------------------------------------------------------ streamed rows
-// RING mode (round 6): long rows.  The row kernel stages a whole block (<= CAP nonzeros) in LDS, so a
-// block of 500-nonzero rows holds 4 rows for its 16 row groups, one wave gathers and the other three idle, and the
-// LDS a CU has (160 KiB) caps the rows it can keep in flight at ~26.  Here every row group owns exactly one virtual
-// row (NG consecutive virtual rows per workgroup, all groups busy) and streams that row's col_idx / values through a
-// per-group LDS slice of CH nonzeros: the lanes of the group load the row's next chunk (16-byte loads through VGPRs,
-// issued before the chunk in LDS is gathered) and write it into the slice after the last gather batch of the
-// current one -- same wave, so no barrier.  A workgroup needs NG x CH x (4 + sizeof(T)) bytes of LDS (24 KiB at
-// K = 32 fp64), whatever the row length.  The gathers and FMAs are the row kernel's (row_dot over the slice), so
-// each row is still ONE fused chain from 0 in CSR order: bit-identical to the reference.  The four groups of a wave
-// run in step over chunk index c (wave-uniform trip count = the longest row of the wave).  vdest as DEST_SPLIT,
-// partial slots stored plainly (the separate combine launch sums them).  One pass over the panel: kw <= G * VEC.
-// U = 32 (SPMM_HIP_RING=2): twice the gathers in flight per row; U = -16 (SPMM_HIP_RING=3): the software-pipelined
-// row (16 to 32 in flight); both at two workgroups per CU (the VGPRs they need).
-template <typename T, int VEC, int G, int U, bool NTC, bool BUF, int MODE, bool XCD>
-__global__ __launch_bounds__(WG, (U > 16 || U < 0) ? 2 : 4) void spmm_ring_kernel(const int32_t *__restrict__ vrow_ptr,
-                                                       const int32_t *__restrict__ col_idx,
-                                                       const T *__restrict__ vals, int nv,
-                                                       const int32_t *__restrict__ vdest, const T *__restrict__ B,
-                                                       T *__restrict__ C, T *__restrict__ P, int ld, int kw,
-                                                       uint32_t b_bytes, int nnz) {
-    static_assert(G >= 4 && G <= 64 && VEC * sizeof(T) == 16, "ring rows: 16-byte lanes, groups of >= 4 lanes");
-    constexpr int NG = WG / G;
-    constexpr int VPI = 16 / (int)sizeof(T);    // values per 16-byte load
-    constexpr int NCL = 2;                      // 16-byte column loads per lane per chunk
-    constexpr int CH = 4 * G * NCL;             // nonzeros per row per chunk
-    constexpr int NVL = CH / (G * VPI);         // 16-byte value loads per lane per chunk
-    using V = vec<T, VEC>;
-    __shared__ __attribute__((aligned(16))) int32_t s_col[NG * CH];
-    __shared__ __attribute__((aligned(16))) T s_val[NG * CH];
-
-    const int b = XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-    if (blockIdx.y > 0) {       // K panels of one launch (plan.ygrid)
-        const uint32_t off = blockIdx.y * (uint32_t)kw;
-        B += off, C += off;
-        b_bytes -= off * (uint32_t)sizeof(T);
-        if (P) P += off;
-    }
-    const int tid = threadIdx.x, grp = tid / G, lane = tid % G;
-    const int v = b * NG + grp;
-    int a = 0, e = 0;
-    if (v < nv) a = vrow_ptr[v], e = vrow_ptr[v + 1];
-    const int cb = a & ~3;                      // 16-byte aligned start of the row's stream
-    int nch = e > a ? (e - cb + CH - 1) / CH : 0;
-#pragma unroll
-    for (int off = G; off < 64; off <<= 1) nch = max(nch, __shfl_xor(nch, off));   // wave-uniform chunk count
-
-    // loads clamped into the padded arrays (the clamped pieces are never read: they lie past every row's end)
-    const int jlc = max(nnz - 1, 0) & ~3, jlv = max(nnz - 1, 0) & ~(VPI - 1);
-    int32_t *my_col = s_col + grp * CH;
-    T *my_val = s_val + grp * CH;
-    i32x4 rc[NCL], rv[NVL];
-    auto load = [&](int c) {
-        const int base = cb + c * CH;
-#pragma unroll
-        for (int i = 0; i < NCL; ++i)
-            rc[i] = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(col_idx + min(base + (i * G + lane) * 4, jlc)));
-#pragma unroll
-        for (int i = 0; i < NVL; ++i)
-            rv[i] = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(vals + min(base + (i * G + lane) * VPI, jlv)));
-    };
-    auto store = [&]() {
-#pragma unroll
-        for (int i = 0; i < NCL; ++i) reinterpret_cast<i32x4 *>(my_col)[i * G + lane] = rc[i];
-#pragma unroll
-        for (int i = 0; i < NVL; ++i) reinterpret_cast<i32x4 *>(my_val)[i * G + lane] = rv[i];
-    };
-
-    const int kk = lane * VEC;
-    const bool live = kk < kw;
-    const BGather<T, VEC, BUF> gather(B, live ? kk : 0, ld, b_bytes);
-    V acc = vzero<T, VEC>();
-    if (nch > 0) {
-        load(0);
-        store();
-    }
-    for (int c = 0; c < nch; ++c) {
-        const bool more = c + 1 < nch;
-        if (more) load(c + 1);
-        const int base = cb + c * CH;
-        const int lo = max(a, base) - base, hi = min(e, base + CH) - base;
-        if (live) acc = row_dot<T, VEC, U>(acc, my_col, my_val, lo, hi, gather);
-        if (more) store();
-    }
-    if (v >= nv || !live) return;
-    T *dst;
-    if constexpr (MODE == DEST_SPLIT) {
-        const int d = vdest[v];
-        dst = (d >= 0) ? C + (size_t)d * ld : P + (size_t)(-d - 1) * ld;
-    } else {
-        dst = C + (size_t)v * ld;
-    }
-    vstore<T, VEC, NTC>(dst + kk, acc);
-}
-
 // ------------------------------------------------------------------------------------------------ LDS B tiles
 // TILE mode: for rows that share their columns -- similar consecutive rows (cross-row similarity) or
 // dense column bands -- the row kernel re-gathers the same B row once per nonzero through L1/L2 (~15 TB/s chip-wide,
