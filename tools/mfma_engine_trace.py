@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--repeat", type=int, default=1, help="timed rounds per (line, K, plan), each on a fresh handle")
+    ap.add_argument("--plan-fields", default="", help="comma list of spmm_hip_debug_plan fields to record per record "
+                    "(host-side plan under the record's environment)")
     args = ap.parse_args()
     import torch
     import spmm_amd as S
@@ -59,9 +61,19 @@ def main():
                     else:
                         os.environ[kk] = vv
                 inf = mf.info()
-                print(json.dumps({"gen": line, "k": k, "plan": name, "dtype": args.dtype,
-                                  "ms": round(e0.elapsed_time(e1) / args.launches, 5),
-                                  "tile": mf.tile_info(), "info": [int(v) for v in inf]}), flush=True)
+                rec = {"gen": line, "k": k, "plan": name, "dtype": args.dtype,
+                       "ms": round(e0.elapsed_time(e1) / args.launches, 5),
+                       "tile": mf.tile_info(), "info": [int(v) for v in inf]}
+                if args.plan_fields:
+                    os.environ.update(env)
+                    dp = S.debug_plan(A.row_ptr, A.col_idx, A.ncols, k, S.F64 if args.dtype == "f64" else S.F32)
+                    rec["plan_fields"] = {f: dp[f] for f in args.plan_fields.split(",")}
+                    for kk, vv in old.items():
+                        if vv is None:
+                            os.environ.pop(kk, None)
+                        else:
+                            os.environ[kk] = vv
+                print(json.dumps(rec), flush=True)
                 mf.close()
             del B, C
 
