@@ -117,7 +117,7 @@ void lane_layout(int kw, int ld, size_t vsize, int &vec, int &g) {
 void free_plan(spmm_hip_t *h) {
     void *ps[] = {h->d_b, h->d_xcol, h->d_c, h->d_part, h->d_vrow_ptr, h->d_vdest, h->d_blk, h->d_long_rows,
                   h->d_wcol, h->d_wval, h->d_lr_cnt, h->d_slot_lr, h->d_tiles, h->d_tchunk, h->d_tcol, h->d_tseg,
-                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm, h->d_mflag, h->d_xw};
+                  h->d_tlidx, h->d_tval, h->d_tstamps, h->d_wperm, h->d_tperm, h->d_mflag};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     h->d_b = h->d_xcol = h->d_c = h->d_part = nullptr;
@@ -131,7 +131,6 @@ void free_plan(spmm_hip_t *h) {
     h->d_tstamps = nullptr;
     h->d_wperm = h->d_tperm = nullptr;
     h->d_mflag = nullptr;
-    h->d_xw = nullptr;
     h->nwperm = h->ntperm = 0;
     h->fuse = false;
     h->win_blk.clear();
@@ -167,21 +166,11 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     // partial slots of this panel as one buffer resource (the fused path needs them below 4 GiB; checked at plan)
     const uint32_t pb = (uint32_t)std::min<uint64_t>((uint64_t)h->nslots * ld * sizeof(T), 0xFFFFFFFFull);
     auto go = [&](auto mode_c, auto xcd_c, auto vl_c, auto pair_c) {
-        auto run = [&](auto xw_c) {
-            spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
-                             decltype(vl_c)::value, decltype(pair_c)::value, decltype(xw_c)::value>
-                <<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
-                h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
-                h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb, h->d_xw);
-        };
-        // LDS x window: B rows of <= 64 bytes (the lane layout of K <= 8 fp64 / 16 fp32), one pass over the panel
-        if constexpr (G * VEC * sizeof(T) <= 64 && U > 0) {
-            if (h->plan.xwin) {
-                run(std::true_type());
-                return;
-            }
-        }
-        run(std::false_type());
+        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
+                         decltype(vl_c)::value, decltype(pair_c)::value>
+            <<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
+            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
+            h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
     };
     using split_c = std::integral_constant<int, DEST_SPLIT>;
     using row_c = std::integral_constant<int, DEST_ROW>;
@@ -741,11 +730,6 @@ constexpr int PAIR_MAX_G = 16;
 constexpr double PAIR_MIN_REUSE = 2.0;
 constexpr int PAIR_WINDOW_ROWS = 16;
 constexpr int64_t PAIR_MIN_NNZ = 4 << 20;
-// LDS x window (spmm_rows_kernel XW): B rows of at most this many bytes (K <= 8 fp64, <= 16 fp32), the
-// policy switch and the share of the row kernel's nonzeros that must sit in windowed blocks
-constexpr double XW_MAX_ROW_BYTES = 64.0;
-constexpr bool XW_POLICY = false;
-constexpr double XW_MIN_FRAC = 0.5;
 constexpr double VL_MIN_ROW = 32.0;   // mean virtual-row length (2 gather batches): tiny matrices stay exact
 
 // XCD-contiguous block order (policy).  The B rows an XCD's L2 must hold at a time are about one row span (the band
@@ -1188,7 +1172,6 @@ struct Draft {
     std::vector<uint8_t> exact;
     MfmaGate gate;
     bool gate_only = false;      // stopped after the matrix-core gate (census mode, no full tile build)
-    std::vector<int2> xw;        // XW mode: per block {first byte of its B span, 16-byte pieces} (0 pieces: none)
 };
 
 // hcol_in: the matrix's columns on the host (nullptr: read from the handle's device copy).  gate_only: stop after
@@ -1478,31 +1461,6 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
             pl.pair_reuse = tile_reuse_sample(h->h_row_ptr.data(), hcol, h->m, h->ncols, INT32_MAX, PAIR_WINDOW_ROWS);
             if (pl.pair_reuse >= PAIR_MIN_REUSE) pl.pair = 1;
         }
-        // LDS x window: at small K, blocks whose nonzeros span few B rows stage that span (B's bytes,
-        // 16-byte aligned, <= XW_BYTES) with the block and gather from LDS.  One launch over one panel of the whole
-        // row (kw == K), B below 2 GiB, no column windows.  SPMM_HIP_XWIN=-1 off, 1 every block that fits.
-        const int env_xw = env_int("SPMM_HIP_XWIN", 0);
-        const double srow_b = (double)pl.kw * (double)h->vsize;
-        const bool xw_ok = W == 0 && pl.kw == k && !pl.ygrid && nnz_rows > 0 && srow_b <= XW_MAX_ROW_BYTES &&
-                           (double)h->ncols * srow_b < 2147483648.0 && !in.blk.empty();
-        if (xw_ok && (env_xw > 0 || (env_xw == 0 && XW_POLICY))) {
-            if (int st = load_cols()) return st;
-            const int64_t rb = (int64_t)pl.kw * (int64_t)h->vsize;
-            d.xw.assign(in.blk.size(), make_int2(0, 0));
-            int64_t nnz_win = 0;
-            for (size_t b = 0; b < in.blk.size(); ++b) {
-                const int2 bk = in.blk[b];
-                const int64_t j0 = in.vrow_ptr[(size_t)bk.x], j1 = in.vrow_ptr[(size_t)(bk.y & BLK_ROWS_MASK)];
-                if (j1 <= j0) continue;
-                int32_t lo = INT32_MAX, hi = -1;
-                for (int64_t j = j0; j < j1; ++j) lo = std::min(lo, hcol[j]), hi = std::max(hi, hcol[j]);
-                const int64_t a0 = ((int64_t)lo * rb) & ~(int64_t)15, a1 = ((int64_t)hi + 1) * rb;
-                const int64_t pieces = (a1 - a0 + 15) / 16;
-                if (pieces * 16 <= XW_BYTES) d.xw[b] = make_int2((int)a0, (int)pieces), nnz_win += j1 - j0;
-            }
-            if (nnz_win > 0 && (env_xw > 0 || (double)nnz_win >= XW_MIN_FRAC * nnz_rows)) pl.xwin = 1;
-            else d.xw.clear();
-        }
     }
     // fused combine: split rows summed by the block that stores their last piece, so no combine
     // launch.  Needs one launch per panel (no column windows), partials below 4 GiB (32-bit buffer offsets) and each
@@ -1556,12 +1514,11 @@ uint64_t plan_fingerprint(const Draft &d) {
     const Plan &p = d.pl;
     const int64_t f[] = {p.k, p.kw, p.npanels, p.ygrid, p.seq_max, p.piece, p.cap, p.block_rows, p.win_cols, p.nwin, p.nseg,
                          p.xcd, p.lmax, p.exact_rows, p.ntile, p.tile_xcd, p.tile_wide, p.tile_mfma, p.tile_rows,
-                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse, p.pair, p.xwin};
+                         p.tile_nnz, p.tile_chunks, (int64_t)d.fuse, p.pair};
     mix(f, sizeof(f));
     mix(d.in.vrow_ptr.data(), d.in.vrow_ptr.size() * 4);
     mix(d.in.vdest.data(), d.in.vdest.size() * 4);
     mix(d.in.blk.data(), d.in.blk.size() * sizeof(int2));
-    mix(d.xw.data(), d.xw.size() * sizeof(int2));
     mix(d.tp.tiles.data(), d.tp.tiles.size() * sizeof(int4));
     mix(d.tp.chunks.data(), d.tp.chunks.size() * sizeof(int4));
     return x;
@@ -1756,7 +1713,6 @@ int spmm_hip_plan(spmm_hip_t *h, int32_t k) {
         if (e == hipSuccess) e = alloc_copy((void **)&h->d_blk, blk4.data(), blk4.size() * sizeof(int4));
     }
     if (e == hipSuccess && !in.vdest.empty()) e = alloc_copy((void **)&h->d_vdest, in.vdest.data(), in.vdest.size() * 4);
-    if (e == hipSuccess && pl.xwin) e = alloc_copy((void **)&h->d_xw, d.xw.data(), d.xw.size() * sizeof(int2));
     if (e == hipSuccess && h->nlong > 0)
         e = alloc_copy((void **)&h->d_long_rows, in.long_rows.data(), in.long_rows.size() * sizeof(int4));
     if (e == hipSuccess && h->fuse) {
@@ -2394,7 +2350,6 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     out[26] = d.gate.tiles;
     out[27] = p.pair;
     out[28] = p.pair_reuse;
-    out[29] = p.xwin;
     return SPMM_HIP_OK;
 }
 

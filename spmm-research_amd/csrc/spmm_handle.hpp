@@ -45,7 +45,6 @@ struct Plan {
     int lmax = 1;              // vector lanes: max groups per row (1 = every row one group, exact)
     int pair = 0;              // 1 = paired short rows: two rows of <= U/2 nonzeros per gather batch (exact)
     double pair_reuse = 0.0;   // the pair policy's sampled 16-row-window reuse (0 = not sampled)
-    int xwin = 0;              // 1 = blocks with a narrow column span gather B from an LDS x window (spmm_rows_kernel XW)
     int64_t exact_rows = 0;    // C rows computed as one left-to-right chain (bit-identical to the reference)
     int ntile = 0;             // LDS B tiles (spmm_tile_kernel), rows and nonzeros they cover, their chunks
     int tile_xcd = 0;          // tiles in XCD-contiguous order
@@ -117,7 +116,6 @@ struct spmm_hip_handle {
     long long *d_tstamps = nullptr;  // SPMM_HIP_TILE_STAMPS=1: per tile {start, end, wait, compute} s_memtime stamps
     int32_t *d_wperm = nullptr;      // window-major position -> nonzero (value updates re-gather wval)
     int32_t *d_tperm = nullptr;      // tile chunk-major position -> nonzero, -1 = padding (value updates re-gather tval)
-    int2 *d_xw = nullptr;            // XW mode: per block {first byte of its B span, 16-byte pieces}
     int *d_mflag = nullptr;          // matrix-core tiles: {A, B} operand outside the exact range (spmm_mfma.hpp)
     int mflag_seq = 0;               // matrix-core launches so far: mflag[1] == seq marks THIS launch's B as out of range
     int64_t nwperm = 0, ntperm = 0;

@@ -85,21 +85,6 @@ struct BGather {
     }
 };
 
-// B row gather from the block's LDS x window (XW mode): the staged image holds B's bytes [xa, xa + n)
-// of the panel, so B row c's lane piece sits at c * row_bytes + lane_off - xa.
-template <typename T, int VEC>
-struct XGather {
-    const char *sx;
-    uint32_t off0;               // lane_off - xa (mod 2^32)
-    uint32_t row_bytes;
-    __device__ __forceinline__ XGather(const char *sx_, int kk, int ld, uint32_t xa)
-        : sx(sx_), off0((uint32_t)kk * (uint32_t)sizeof(T) - xa), row_bytes((uint32_t)ld * (uint32_t)sizeof(T)) {}
-    __device__ __forceinline__ vec<T, VEC> operator()(int c) const {
-        return *reinterpret_cast<const vec<T, VEC> *>(sx + ((uint32_t)c * row_bytes + off0));
-    }
-};
-constexpr int XW_BYTES = 16384;                // LDS x window of one block (XW mode)
-
 // Software-pipelined row (tuning build: U < 0 selects it with |U| per batch): batch j+1's gathers are issued before
 // batch j's FMAs, so between |U| and 2|U| gathers stay in flight instead of U then none; same FMA order.
 template <typename T, int VEC, int U, typename Gather>
@@ -338,11 +323,8 @@ __device__ __forceinline__ bool rows_pair_step(const int32_t *s_rp, const int32_
     return true;
 }
 
-// XW (round 6; small K): blocks whose nonzeros' columns span few enough B rows (xw[b] = {first byte of
-// the span in the panel, 16-byte aligned; its length in 16-byte pieces}, pieces > 0) stage that piece of B in LDS with
-// the block and gather from LDS; other blocks (pieces == 0) gather from L2 as before.  Same values, same FMA chain.
 template <typename T, int VEC, int G, int U, int CAP, bool NTC, bool DMA, bool BUF, int MODE, bool XCD = false,
-          bool VL = false, bool PAIR = false, bool XW = false>
+          bool VL = false, bool PAIR = false>
 __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restrict__ vrow_ptr,
                                                        const int32_t *__restrict__ col_idx,
                                                        const T *__restrict__ vals,
@@ -352,12 +334,10 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
                                                        int ld, int kw, uint32_t b_bytes, int lmax,
                                                        int32_t *__restrict__ lr_cnt,
                                                        const int32_t *__restrict__ slot_lr,
-                                                       const int4 *__restrict__ long_rows, uint32_t p_bytes,
-                                                       const int2 *__restrict__ xw = nullptr) {
+                                                       const int4 *__restrict__ long_rows, uint32_t p_bytes) {
     constexpr int SVN = 16 / (int)sizeof(T);
     constexpr int CAPP = CAP + 4;                         // staged window starts at a 16-byte boundary
     __shared__ __attribute__((aligned(16))) int32_t s_rp[CAP_ROWS + 64];
-    __shared__ __attribute__((aligned(16))) char s_x[XW ? XW_BYTES : 16];
     __shared__ __attribute__((aligned(16))) int32_t s_col[CAPP];
     __shared__ __attribute__((aligned(16))) T s_val[CAPP];
     using V = vec<T, VEC>;
@@ -437,23 +417,6 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
         for (int u = 0; u < NR; ++u)
             if (tid + u * WG <= nrows) s_rp[tid + u * WG] = rp[u];
     }
-    int2 xwin = make_int2(0, 0);
-    if constexpr (XW) {
-        xwin = xw[b];                                       // block-uniform
-        if (xwin.y > 0) {
-            // B's bytes [xa, xa + 16 * pieces) of this panel (buffer loads: a piece past B's end reads 0, never used)
-            const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void *)B, (short)0, (int)b_bytes, 0x00020000);
-            constexpr int NXP = XW_BYTES / 16 / WG;
-            i32x4 xb[NXP];
-#pragma unroll
-            for (int u = 0; u < NXP; ++u)
-                if (tid + u * WG < xwin.y)
-                    xb[u] = __builtin_amdgcn_raw_buffer_load_b128(brs, (uint32_t)xwin.x + 16u * (uint32_t)(tid + u * WG), 0, 0);
-#pragma unroll
-            for (int u = 0; u < NXP; ++u)
-                if (tid + u * WG < xwin.y) reinterpret_cast<i32x4 *>(s_x)[tid + u * WG] = xb[u];
-        }
-    }
     __syncthreads();
 #ifdef SPMM_STAMPS
     const long long st_staged = __builtin_amdgcn_s_memrealtime();
@@ -475,7 +438,10 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
     const bool fuse = MODE == DEST_SPLIT && lr_cnt != nullptr;
     __amdgpu_buffer_rsrc_t prs;
     if (MODE == DEST_SPLIT) prs = __builtin_amdgcn_make_buffer_rsrc((void *)P, (short)0, (int)p_bytes, 0x00020000);
-    auto rows = [&](const int kk, const auto &gather) {
+    for (int kc = 0; kc < kw; kc += G * VEC) {
+        const int kk = kc + lane * VEC;
+        if (kk >= kw) continue;
+        const BGather<T, VEC, BUF> gather(B, kk, ld, b_bytes);
         if constexpr (PAIR && MODE != DEST_CHAIN && U > 1) if (L == 1) {   // L: block-uniform (vector-lane blocks below)
             auto init = [&](int) { return vzero<T, VEC>(); };
             auto store_row = [&](int r, const vec<T, VEC> &acc) {
@@ -497,7 +463,7 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
                     store_row(r2, row_dot<T, VEC, U>(vzero<T, VEC>(), s_col, s_val, s_rp[r2] - jb, s_rp[r2 + 1] - jb,
                                                      gather));
             }
-            return;
+            continue;
         }
         for (int r = grp; r < nrows; r += rstep) {
             T *dst;
@@ -531,17 +497,6 @@ __global__ __launch_bounds__(WG, 4) void spmm_rows_kernel(const int32_t *__restr
                 else vstore<T, VEC, NTC>(dst + kk, acc);
             }
         }
-    };
-    for (int kc = 0; kc < kw; kc += G * VEC) {
-        const int kk = kc + lane * VEC;
-        if (kk >= kw) continue;
-        if constexpr (XW) {
-            if (xwin.y > 0) {            // block-uniform; the host allows XW only for one pass over the panel
-                rows(kk, XGather<T, VEC>(s_x, kk, ld, (uint32_t)xwin.x));
-                continue;
-            }
-        }
-        rows(kk, BGather<T, VEC, BUF>(B, kk, ld, b_bytes));
     }
 
 #ifdef SPMM_STAMPS
