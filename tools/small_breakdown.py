@@ -100,6 +100,11 @@ def main():
                    "compute_us": round(float(np.median(comp)), 2), "compute_p90_us": round(float(np.percentile(comp, 90)), 2),
                    "compute_max_us": round(float(comp.max()), 2),
                    "tail_us": round(float(done.max() - np.percentile(done, 90)), 2),
+                   # mean blocks in flight per CU over the span, and the block that ends the launch
+                   "active_blocks_per_cu": round(float((done - start).sum() / max(done.max(), 1e-9) / 256), 2),
+                   "last_block_start_us": round(float(start[np.argmax(done)]), 2),
+                   "last_block_compute_us": round(float(comp[np.argmax(done)]), 2),
+                   "max_row_nnz": int(np.diff(A.row_ptr).max()),
                    "tiles": int(info[19]), "split_rows": int(info[6]), "lmax": int(info[16]), "cap": int(info[9]),
                    "seq_max": int(info[8]), "panel_k": int(info[10]), "windows": int(info[12])}
             print(json.dumps(rec), flush=True)
