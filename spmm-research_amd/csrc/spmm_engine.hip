@@ -58,6 +58,7 @@ namespace {
     } while (0)
 
 constexpr int CAP = 2048;         // LDS capacity of a block (nonzeros)
+constexpr int CAP_BIG = 4096;     // the wide window: SPMM_HIP_CAP=4096, 16-byte lanes, groups of >= 8 lanes
 constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may read up to 3 elements past nnz)
 // LDS B tiles (spmm_tile_kernel)
 #ifndef SPMM_TILE_UCB_KB
@@ -166,11 +167,21 @@ void launch_rows_v(spmm_hip_t *h, const T *B, T *C, T *P, int ld, int kw, hipStr
     // partial slots of this panel as one buffer resource (the fused path needs them below 4 GiB; checked at plan)
     const uint32_t pb = (uint32_t)std::min<uint64_t>((uint64_t)h->nslots * ld * sizeof(T), 0xFFFFFFFFull);
     auto go = [&](auto mode_c, auto xcd_c, auto vl_c, auto pair_c) {
-        spmm_rows_kernel<T, VEC, G, U, CAP, NTC, DMA, BUF, decltype(mode_c)::value, decltype(xcd_c)::value,
-                         decltype(vl_c)::value, decltype(pair_c)::value>
-            <<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
-            h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
-            h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
+        auto run = [&](auto cap_c) {
+            spmm_rows_kernel<T, VEC, G, U, decltype(cap_c)::value, NTC, DMA, BUF, decltype(mode_c)::value,
+                             decltype(xcd_c)::value, decltype(vl_c)::value, decltype(pair_c)::value>
+                <<<dim3(h->nblk, h->plan.ygrid ? h->plan.npanels : 1), WG, 0, s>>>(
+                h->d_vrow_ptr, h->d_col, (const T *)h->d_val, h->d_blk, h->nblk, h->d_vdest, B, C, P, ld, kw, bb,
+                h->plan.lmax, h->fuse ? h->d_lr_cnt : nullptr, h->d_slot_lr, h->d_long_rows, pb);
+        };
+        // the wide window (blocks of up to CAP_BIG nonzeros): 16-byte lanes, groups of >= 8 lanes, no pairing
+        if constexpr (VEC * sizeof(T) == 16 && G >= 8 && !decltype(pair_c)::value && U > 0) {
+            if (h->plan.cap > CAP) {
+                run(std::integral_constant<int, CAP_BIG>());
+                return;
+            }
+        }
+        run(std::integral_constant<int, CAP>());
     };
     using split_c = std::integral_constant<int, DEST_SPLIT>;
     using row_c = std::integral_constant<int, DEST_ROW>;
@@ -1235,8 +1246,10 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
     // block capacity: the LDS window (CAP), smaller for small matrices so >= ~1024 blocks exist (a 4096-nonzero
     // window for one-lane row groups measured slower at K = 1, §6.2)
     const int cap_env = env_int("SPMM_HIP_CAP", 0);
+    // the wide window CAP_BIG only where its kernel exists (16-byte lanes, groups of >= 8 lanes, one launch per panel)
+    const bool big_ok = vec * (int)h->vsize == 16 && g >= 8;
     pl.cap = h->var.cap > 0 ? std::min(h->var.cap, CAP)
-             : cap_env > 0   ? std::min(cap_env, CAP)
+             : cap_env > 0   ? std::min(cap_env, (cap_env > CAP && big_ok) ? CAP_BIG : CAP)
                              : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
     const int seq_env = env_int("SPMM_HIP_SEQ_MAX", 0);
     pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max : seq_env > 0 ? seq_env : split_length(h, pl.kw);
@@ -1364,7 +1377,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
             if (int st = load_cols()) return st;
         }
         pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
-        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) &&
+        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) && pl.cap <= CAP &&
             rows_sorted(h->h_row_ptr.data(), hcol, h->m)) {
             std::vector<Piece> pcs;
             Inspection tmp;
@@ -1452,7 +1465,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
         // still in step.  No column windows, row groups of >= 2 lanes (one-lane groups hold 1-2 rows of a block);
         // blocks that take vector lanes keep their loop.  SPMM_HIP_PAIR=-1 off, 1 forced.
         const int env_pair = env_int("SPMM_HIP_PAIR", 0);
-        const bool pair_ok = W == 0 && g >= 2 && nnz_rows > 0;
+        const bool pair_ok = W == 0 && g >= 2 && nnz_rows > 0 && pl.cap <= CAP;
         if (pair_ok && env_pair > 0)
             pl.pair = 1;
         else if (pair_ok && env_pair == 0 && h->vsize == 8 && g <= PAIR_MAX_G && h->nnz >= PAIR_MIN_NNZ &&
