@@ -263,7 +263,8 @@ void spmm_hip_debug_tiles_free(spmm_hip_tiles_t *t);
  * [15] nonzeros in tiles, [16] chunks, [17] row-kernel blocks, [18] split rows, [19] exact rows, [20] vector lanes,
  * [21] XCD order, [22] column windows, [23] 1 = gate only, [24]/[25] plan fingerprint (low / high 32 bits; two
  * plans are the same exactly when these agree), [26] est. taken tiles, [27] paired short rows,
- * [28] the pair policy's sampled reuse of 16-row windows (0 = not sampled). */
+ * [28] the pair policy's sampled reuse of 16-row windows (0 = not sampled), [29] block capacity (nonzeros; 4096 =
+ * the wide window). */
 #define SPMM_HIP_PLAN_SLOTS 32
 int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t m, int64_t ncols, int32_t k,
                         int32_t dtype, int32_t mfma, int32_t gate_only, double *out);

@@ -59,6 +59,8 @@ namespace {
 
 constexpr int CAP = 2048;         // LDS capacity of a block (nonzeros)
 constexpr int CAP_BIG = 4096;     // the wide window: SPMM_HIP_CAP=4096, 16-byte lanes, groups of >= 8 lanes
+constexpr int64_t WIDE_MIN_NNZ = 2500000;   // policy: the wide window for fp64 matrices this large ...
+constexpr double WIDE_MIN_ROW = 256.0;      // ... whose rows average this many nonzeros (§6.43)
 constexpr int PAD_BYTES = 64;     // device col/val padding (16-byte staging may read up to 3 elements past nnz)
 // LDS B tiles (spmm_tile_kernel)
 #ifndef SPMM_TILE_UCB_KB
@@ -1247,9 +1249,15 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
     // window for one-lane row groups measured slower at K = 1, §6.2)
     const int cap_env = env_int("SPMM_HIP_CAP", 0);
     // the wide window CAP_BIG only where its kernel exists (16-byte lanes, groups of >= 8 lanes, one launch per panel)
+    // Policy: fp64 matrices of >= WIDE_MIN_NNZ nonzeros whose rows average >= WIDE_MIN_ROW take the
+    // wide window unless column windows or tiles are chosen below (both lower it back to CAP).
     const bool big_ok = vec * (int)h->vsize == 16 && g >= 8;
+    const double avg_nnz_row = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    const bool wide = big_ok && h->vsize == 8 && k == 32 && pl.kw == 32 && h->nnz >= WIDE_MIN_NNZ &&
+                      avg_nnz_row >= WIDE_MIN_ROW;      // measured at K = 32 fp64 only (K = 128 lost, §6.43)
     pl.cap = h->var.cap > 0 ? std::min(h->var.cap, CAP)
              : cap_env > 0   ? std::min(cap_env, (cap_env > CAP && big_ok) ? CAP_BIG : CAP)
+             : wide          ? CAP_BIG
                              : std::max(256, std::min(CAP, pow2_ceil(h->nnz / 1024)));
     const int seq_env = env_int("SPMM_HIP_SEQ_MAX", 0);
     pl.seq_max = h->var.seq_max > 0 ? h->var.seq_max : seq_env > 0 ? seq_env : split_length(h, pl.kw);
@@ -1377,7 +1385,7 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
             if (int st = load_cols()) return st;
         }
         pl.xcd = xcd_order(h, srow, span, pl.cap) ? 1 : 0;
-        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) && pl.cap <= CAP &&
+        if (!tiles && maybe_win && forced >= 0 && (forced > 0 || !pl.xcd) &&
             rows_sorted(h->h_row_ptr.data(), hcol, h->m)) {
             std::vector<Piece> pcs;
             Inspection tmp;
@@ -1385,6 +1393,9 @@ int draft_plan(const spmm_hip_t *h, int k, const int32_t *hcol_in, bool gate_onl
             W = window_cols(h, pl.kw, pcs, hcol, h->var.win_bytes, crs, &pl.nseg);
         }
     }
+    // the wide window only for the plain row kernel: column windows (chained mode) and the tiles' leftover rows keep
+    // the default one (the wide window measured 0.70-0.82x where it displaced column windows, §6.43)
+    if ((W > 0 || tiles) && pl.cap > CAP) pl.cap = CAP;
     if (W > 0) {
         pl.xcd = 0;
         inspect_windows(h->h_row_ptr.data(), hcol, h->m, h->ncols, pl.seq_max, pl.cap, W, in, pl.block_rows);
@@ -2363,6 +2374,7 @@ int spmm_hip_debug_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t 
     out[26] = d.gate.tiles;
     out[27] = p.pair;
     out[28] = p.pair_reuse;
+    out[29] = p.cap;
     return SPMM_HIP_OK;
 }
 

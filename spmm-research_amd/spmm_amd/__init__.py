@@ -385,7 +385,7 @@ PLAN_SLOTS = 32     # SPMM_HIP_PLAN_SLOTS
 PLAN_FIELDS = ("mode", "gate", "r16", "take", "est_tile_nnz", "est_chunks", "max_chunks", "t_on_us", "t_off_us",
                "sampled", "seq_max", "piece", "kw", "npanels", "ntile", "tile_nnz", "tile_chunks", "blocks",
                "split_rows", "exact_rows", "lmax", "xcd", "nwin", "gate_only", "fp_lo", "fp_hi", "est_tiles", "pair",
-               "pair_reuse")
+               "pair_reuse", "cap")
 GATE_SAMPLE = ("sampled", "r16", "take", "est_tiles", "est_tile_nnz", "est_chunks", "max_chunks")
 
 
