@@ -28,10 +28,7 @@ def bits(a):
 
 
 def run(S, A, vals, x, k, cap, monkeypatch, extra=None):
-    if cap:
-        monkeypatch.setenv("SPMM_HIP_CAP", str(cap))
-    else:
-        monkeypatch.delenv("SPMM_HIP_CAP", raising=False)
+    monkeypatch.setenv("SPMM_HIP_CAP", str(cap or 2048))   # 2048: the default window (the policy may pick 4096)
     for kk, vv in (extra or {}).items():
         monkeypatch.setenv(kk, vv)
     mf = S.csr_to_format(A.row_ptr, A.col_idx, vals, A.m, A.ncols, A.nnz, k, 0)
